@@ -1,0 +1,250 @@
+"""ctypes front-end of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+`OracleOSQP` mirrors the `osqp.OSQP` Python object exactly as the reference uses it
+(reference src/trajectorySimulate.py:242-245 setup, :296 solve, :342/:348 update), on top of the
+C restatement in osqp_oracle.c.  Only tests/, bench.py's cpu_baseline leg and
+__graft_entry__.smoke() may import this module; the product (mpc_arpo_project_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from types import SimpleNamespace
+
+import numpy as np
+import scipy.sparse as sp
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libosqp_oracle.so")
+
+STATUS_STRINGS = {
+    1: "solved",
+    2: "solved inaccurate",
+    3: "primal infeasible inaccurate",
+    4: "dual infeasible inaccurate",
+    -2: "maximum iterations reached",
+    -3: "primal infeasible",
+    -4: "dual infeasible",
+    -5: "interrupted",
+    -6: "run time limit reached",
+    -7: "problem non convex",
+    -10: "unsolved",
+}
+OSQP_INFTY = 1e30
+
+
+class Settings(C.Structure):
+    _fields_ = [
+        ("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double),
+        ("eps_abs", C.c_double), ("eps_rel", C.c_double),
+        ("eps_prim_inf", C.c_double), ("eps_dual_inf", C.c_double),
+        ("delta", C.c_double), ("adaptive_rho_tolerance", C.c_double),
+        ("max_iter", C.c_int), ("scaling", C.c_int), ("adaptive_rho", C.c_int),
+        ("adaptive_rho_interval", C.c_int), ("polish", C.c_int),
+        ("polish_refine_iter", C.c_int), ("check_termination", C.c_int),
+        ("warm_start", C.c_int), ("scaled_termination", C.c_int),
+    ]
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with the committed Makefile (gcc)."""
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(_LIB_PATH)
+        dp, ip, vp = C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_void_p
+        L.oqp_default_settings.argtypes = [C.POINTER(Settings)]
+        L.oqp_setup.restype = vp
+        L.oqp_setup.argtypes = [C.c_int, C.c_int, ip, ip, dp, dp, ip, ip, dp, dp, dp,
+                                C.POINTER(Settings), ip]
+        for name in ("oqp_cleanup",):
+            getattr(L, name).argtypes = [vp]
+        L.oqp_update_lin_cost.argtypes = [vp, dp]
+        L.oqp_update_bounds.argtypes = [vp, dp, dp]
+        L.oqp_update_A.argtypes = [vp, dp]
+        L.oqp_update_rho.argtypes = [vp, C.c_double]
+        L.oqp_warm_start.argtypes = [vp, dp, dp]
+        L.oqp_solve.argtypes = [vp]
+        L.oqp_get_x.argtypes = [vp, dp]
+        L.oqp_get_y.argtypes = [vp, dp]
+        for name in ("oqp_status", "oqp_iter", "oqp_status_polish", "oqp_rho_updates",
+                     "oqp_nnz_L"):
+            getattr(L, name).argtypes = [vp]
+            getattr(L, name).restype = C.c_int
+        for name in ("oqp_obj_val", "oqp_pri_res", "oqp_dua_res", "oqp_rho"):
+            getattr(L, name).argtypes = [vp]
+            getattr(L, name).restype = C.c_double
+        L.oqp_get_state.argtypes = [vp, dp, dp, dp, dp, dp, dp]
+        L.oqp_batch_solve.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip, dp, dp, ip, ip, dp,
+                                      dp, dp, C.POINTER(Settings), C.c_int, dp, dp, ip, ip]
+        L.oqp_batch_solve.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def make_settings(**kw) -> Settings:
+    s = Settings()
+    lib().oqp_default_settings(C.byref(s))
+    for k, v in kw.items():
+        if k == "verbose":
+            continue
+        if not hasattr(s, k):
+            raise ValueError(f"unknown setting {k}")
+        setattr(s, k, type(getattr(s, k))(v))
+    return s
+
+
+def prepare_P(P):
+    """osqp utils.prepare_data: triu if not upper, CSC, sorted indices."""
+    P = sp.csc_matrix(P)
+    if sp.tril(P, -1).nnz > 0 or sp.tril(P, -1).data.size > 0:
+        P = sp.triu(P, format="csc")
+    P = sp.csc_matrix(P)
+    if not P.has_sorted_indices:
+        P.sort_indices()
+    return P
+
+
+def prepare_A(A):
+    A = sp.csc_matrix(A)
+    if not A.has_sorted_indices:
+        A.sort_indices()
+    return A
+
+
+class OracleOSQP:
+    """Drop-in of the osqp 0.6 Python object for the calls the reference makes."""
+
+    def __init__(self):
+        self._w = None
+
+    def setup(self, P, q, A, l, u, **settings):
+        L = lib()
+        P = prepare_P(P)
+        A = prepare_A(A)
+        self.n, self.m = P.shape[0], A.shape[0]
+        self._Pp = np.ascontiguousarray(P.indptr, dtype=np.int32)
+        self._Pi = np.ascontiguousarray(P.indices, dtype=np.int32)
+        self._Px = np.ascontiguousarray(P.data, dtype=np.float64)
+        self._Ap = np.ascontiguousarray(A.indptr, dtype=np.int32)
+        self._Ai = np.ascontiguousarray(A.indices, dtype=np.int32)
+        Ax = np.ascontiguousarray(A.data, dtype=np.float64)
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        l = np.ascontiguousarray(np.maximum(l, -OSQP_INFTY), dtype=np.float64)
+        u = np.ascontiguousarray(np.minimum(u, OSQP_INFTY), dtype=np.float64)
+        self.settings = make_settings(**settings)
+        err = C.c_int(0)
+        self._w = L.oqp_setup(self.n, self.m, _ip(self._Pp), _ip(self._Pi), _dp(self._Px),
+                              _dp(q), _ip(self._Ap), _ip(self._Ai), _dp(Ax), _dp(l), _dp(u),
+                              C.byref(self.settings), C.byref(err))
+        if not self._w:
+            raise ValueError(f"oracle setup failed (code {err.value})")
+        self.nnzA = int(self._Ap[-1])
+
+    def update(self, q=None, l=None, u=None, Px=None, Ax=None, Ax_idx=None):
+        L = lib()
+        if Px is not None:
+            raise NotImplementedError("Px updates are not used by the reference")
+        if q is not None:
+            q = np.ascontiguousarray(q, dtype=np.float64)
+            if q.shape != (self.n,):
+                raise ValueError("q must have length n")
+            L.oqp_update_lin_cost(self._w, _dp(q))
+        if l is not None or u is not None:
+            if l is None or u is None:
+                raise NotImplementedError("one-sided bound updates are not used by the reference")
+            l = np.ascontiguousarray(np.maximum(l, -OSQP_INFTY), dtype=np.float64)
+            u = np.ascontiguousarray(np.minimum(u, OSQP_INFTY), dtype=np.float64)
+            if l.shape != (self.m,) or u.shape != (self.m,):
+                raise ValueError("l and u must have length m")
+            if L.oqp_update_bounds(self._w, _dp(l), _dp(u)):
+                raise ValueError("lower bound must be lower than or equal to upper bound")
+        if Ax is not None:
+            if Ax_idx is not None and len(Ax_idx):
+                raise NotImplementedError("indexed Ax updates are not used by the reference")
+            Ax = np.ascontiguousarray(Ax, dtype=np.float64)
+            if Ax.shape != (self.nnzA,):
+                raise ValueError("Ax must have nnz(A) entries")
+            if L.oqp_update_A(self._w, _dp(Ax)):
+                raise ValueError("KKT refactorization failed")
+
+    def update_settings(self, **kw):
+        raise NotImplementedError
+
+    def warm_start(self, x=None, y=None):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        lib().oqp_warm_start(self._w, _dp(x), _dp(y))
+
+    def solve(self):
+        L = lib()
+        L.oqp_solve(self._w)
+        x = np.empty(self.n)
+        y = np.empty(self.m)
+        L.oqp_get_x(self._w, _dp(x))
+        L.oqp_get_y(self._w, _dp(y))
+        st = L.oqp_status(self._w)
+        info = SimpleNamespace(
+            status=STATUS_STRINGS[st], status_val=st, iter=L.oqp_iter(self._w),
+            obj_val=L.oqp_obj_val(self._w), pri_res=L.oqp_pri_res(self._w),
+            dua_res=L.oqp_dua_res(self._w), rho_estimate=L.oqp_rho(self._w),
+            rho_updates=L.oqp_rho_updates(self._w), status_polish=L.oqp_status_polish(self._w))
+        return SimpleNamespace(x=x, y=y, info=info)
+
+    def state(self):
+        """scaled iterates (x, z, y), scaling (D, E, c) and rho -- white-box test hook"""
+        xs, zs, ys = np.empty(self.n), np.empty(self.m), np.empty(self.m)
+        D, E, c = np.empty(self.n), np.empty(self.m), C.c_double(0)
+        lib().oqp_get_state(self._w, _dp(xs), _dp(zs), _dp(ys), _dp(D), _dp(E), C.byref(c))
+        return dict(x=xs, z=zs, y=ys, D=D, E=E, c=c.value, rho=lib().oqp_rho(self._w),
+                    nnzL=lib().oqp_nnz_L(self._w))
+
+    def __del__(self):
+        if getattr(self, "_w", None) and _lib is not None:
+            _lib.oqp_cleanup(self._w)
+            self._w = None
+
+
+def batch_solve(P, q, A_pattern, Ax_batch, l_batch, u_batch, nthreads=1, **settings):
+    """Cold-solve B instances sharing P, q and the sparsity of A (CPU baseline driver)."""
+    L = lib()
+    P = prepare_P(P)
+    A = prepare_A(A_pattern)
+    n, m = P.shape[0], A.shape[0]
+    B = Ax_batch.shape[0]
+    Pp, Pi = P.indptr.astype(np.int32), P.indices.astype(np.int32)
+    Ap, Ai = A.indptr.astype(np.int32), A.indices.astype(np.int32)
+    Px = np.ascontiguousarray(P.data, dtype=np.float64)
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    Ax_batch = np.ascontiguousarray(Ax_batch, dtype=np.float64)
+    l_batch = np.ascontiguousarray(np.maximum(l_batch, -OSQP_INFTY), dtype=np.float64)
+    u_batch = np.ascontiguousarray(np.minimum(u_batch, OSQP_INFTY), dtype=np.float64)
+    s = make_settings(**settings)
+    x = np.empty((B, n))
+    y = np.empty((B, m))
+    st = np.empty(B, dtype=np.int32)
+    it = np.empty(B, dtype=np.int32)
+    rc = L.oqp_batch_solve(B, n, m, _ip(Pp), _ip(Pi), _dp(Px), _dp(q), _ip(Ap), _ip(Ai),
+                           _dp(Ax_batch), _dp(l_batch), _dp(u_batch), C.byref(s), nthreads,
+                           _dp(x), _dp(y), _ip(st), _ip(it))
+    if rc:
+        raise RuntimeError(f"oracle batch solve failed ({rc})")
+    return x, y, st, it

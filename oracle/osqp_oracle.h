@@ -1,0 +1,97 @@
+/*
+ * osqp_oracle.h -- TEST INFRASTRUCTURE ONLY (the parity checker and the CPU baseline).
+ *
+ * A plain-C restatement of the OSQP 0.6.x operator-splitting QP solver, which is the arithmetic
+ * behind the reference's hot path (`osqp.OSQP().setup/solve/update`, called at
+ * reference src/trajectorySimulate.py:242-245,296,342,348 and src/trajectorySimulateC.py:269-272,
+ * 338,399,405).  OSQP itself is a third-party dependency that the reference neither vendors nor
+ * pins (no requirements file; the `warm_start=`/`verbose=` keyword names point at the 0.6 series)
+ * and it is not installed in this image, so this file restates its published algorithm
+ * (Stellato et al., Math. Prog. Comp. 2020, Alg. 1, and the 0.6 C sources' structure: scaling.c
+ * scale_data/unscale_data, auxil.c set_rho_vec/update_rho_vec/compute_rho_estimate/
+ * update_xz_tilde/update_x/update_z/update_y/check_termination/is_primal_infeasible/
+ * is_dual_infeasible/store_solution, polish.c, kkt.c form_KKT, qdldl.c etree/factor/solve).
+ *
+ * Deliberate, documented deviations (see DESIGN.md "Oracle"):
+ *   - fill-reducing ordering: an exact minimum-degree ordering written here instead of
+ *     SuiteSparse AMD (changes rounding only; L and D are the unique LDL^T of the permuted KKT);
+ *   - adaptive-rho interval: OSQP's non-PROFILING rule, 4 x check_termination = 100 iterations,
+ *     instead of the wall-clock rule of PROFILING builds (which is non-deterministic).
+ *
+ * Nothing under mpc_arpo_project_amd/ may link or call this library; only tests/, bench.py's
+ * cpu_baseline leg and __graft_entry__.smoke() use it, as the checker.
+ */
+#ifndef OSQP_ORACLE_H
+#define OSQP_ORACLE_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status values: OSQP 0.6 constants.h */
+#define OQP_SOLVED 1
+#define OQP_SOLVED_INACCURATE 2
+#define OQP_PRIMAL_INFEASIBLE_INACCURATE 3
+#define OQP_DUAL_INFEASIBLE_INACCURATE 4
+#define OQP_MAX_ITER_REACHED (-2)
+#define OQP_PRIMAL_INFEASIBLE (-3)
+#define OQP_DUAL_INFEASIBLE (-4)
+#define OQP_NON_CVX (-7)
+#define OQP_UNSOLVED (-10)
+
+#define OQP_INFTY 1e30
+
+typedef struct {
+  double rho, sigma, alpha;
+  double eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
+  double delta;                  /* polish regularization */
+  double adaptive_rho_tolerance;
+  int max_iter, scaling, adaptive_rho, adaptive_rho_interval;
+  int polish, polish_refine_iter, check_termination, warm_start, scaled_termination;
+} oqp_settings;
+
+typedef struct oqp_work oqp_work;
+
+void oqp_default_settings(oqp_settings *s);
+
+/* P: upper-triangular CSC (n x n), A: CSC (m x n). Inputs are copied. l/u may contain +-inf
+ * (clipped to +-OQP_INFTY as the osqp Python wrapper does).  err != 0 on failure. */
+oqp_work *oqp_setup(int n, int m, const int *Pp, const int *Pi, const double *Px, const double *q,
+                    const int *Ap, const int *Ai, const double *Ax, const double *l,
+                    const double *u, const oqp_settings *s, int *err);
+void oqp_cleanup(oqp_work *w);
+
+int oqp_update_lin_cost(oqp_work *w, const double *q);
+int oqp_update_bounds(oqp_work *w, const double *l, const double *u);
+int oqp_update_A(oqp_work *w, const double *Ax); /* all nnz(A) values, CSC order */
+int oqp_update_rho(oqp_work *w, double rho);
+int oqp_warm_start(oqp_work *w, const double *x, const double *y);
+int oqp_solve(oqp_work *w);
+
+/* results of the last solve */
+void oqp_get_x(const oqp_work *w, double *x);
+void oqp_get_y(const oqp_work *w, double *y);
+int oqp_status(const oqp_work *w);
+int oqp_iter(const oqp_work *w);
+int oqp_status_polish(const oqp_work *w);
+int oqp_rho_updates(const oqp_work *w);
+double oqp_obj_val(const oqp_work *w);
+double oqp_pri_res(const oqp_work *w);
+double oqp_dua_res(const oqp_work *w);
+double oqp_rho(const oqp_work *w);
+int oqp_nnz_L(const oqp_work *w);
+/* expose the solver's scaled iterates (warm-start state) and scaling, for white-box tests */
+void oqp_get_state(const oqp_work *w, double *x_s, double *z_s, double *y_s, double *D, double *E,
+                   double *c);
+
+/* Batch driver used as the CPU baseline and by the parity tests: for each instance b, set up a
+ * solver on (P, q, A with values Ax[b], l[b], u[b]), solve it (cold), and store x/y/status/iter.
+ * Instances are spread over `nthreads` POSIX threads.  Returns 0 on success. */
+int oqp_batch_solve(int B, int n, int m, const int *Pp, const int *Pi, const double *Px,
+                    const double *q, const int *Ap, const int *Ai, const double *Ax_batch,
+                    const double *l_batch, const double *u_batch, const oqp_settings *s,
+                    int nthreads, double *x_out, double *y_out, int *status_out, int *iter_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
