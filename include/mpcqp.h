@@ -1,0 +1,140 @@
+/*
+ * mpcqp.h -- C ABI of libmpcqp.so, the MI355X-native batched MPC-QP engine.
+ *
+ * This is the drop-in boundary for the reference's hot path: the OSQP object that
+ * src/trajectorySimulate.py / src/trajectorySimulateC.py create, set up and drive every control
+ * step.  Each entry point replaces one OSQP call the reference makes (OSQP 0.6 C names in
+ * brackets; the Python wrapper methods the reference calls are what a binding maps onto them):
+ *
+ *   mpcqp_create + mpcqp_set_data  <- osqp.OSQP(); prob.setup(P, q, A, l, u, warm_start=True,
+ *                                     verbose=False)  [osqp_setup]
+ *                                     reference src/trajectorySimulate.py:242-245,
+ *                                               src/trajectorySimulateC.py:269-272
+ *   mpcqp_update_bounds            <- prob.update(l=l, u=u)  [osqp_update_bounds]
+ *                                     reference src/trajectorySimulate.py:342,
+ *                                               src/trajectorySimulateC.py:399
+ *   mpcqp_update_A (+ bounds)      <- prob.update(Ax=A.data, l=l, u=u)
+ *                                     [osqp_update_bounds + osqp_update_A]
+ *                                     reference src/trajectorySimulate.py:348,
+ *                                               src/trajectorySimulateC.py:405
+ *   mpcqp_solve                    <- res = prob.solve()  [osqp_solve]; the caller reads
+ *                                     res.x[(Nx+1)*nx:(Nx+1)*nx+nu] and res.info.status
+ *                                     reference src/trajectorySimulate.py:296-314,
+ *                                               src/trajectorySimulateC.py:338-356
+ *   mpcqp_warm_start               <- prob.warm_start(x=, y=)  [osqp_warm_start]
+ *   mpcqp_destroy                  <- object destruction  [osqp_cleanup]
+ *
+ * Differences from OSQP by design: one handle holds a BATCH of B independent QPs that share the
+ * sparsity pattern of P and A (and the values of P and q); A values and the bounds l, u are per
+ * instance.  B = 1 is the reference's use.
+ *
+ * Rules
+ *   - every function returns 0 on success and a negative MPCQP_E* code on failure; nothing throws
+ *     across the ABI; mpcqp_last_error() gives a message for the calling thread;
+ *   - structure arrays (mpcqp_structure) are HOST pointers read during mpcqp_create only;
+ *   - every data pointer is a DEVICE pointer owned by the caller (e.g. a torch tensor's
+ *     data_ptr()), laid out row-major [instance][element], float64 / int32;
+ *   - work is enqueued on the HIP stream given to mpcqp_create and is asynchronous with respect to
+ *     the host: synchronise the stream before reading outputs;
+ *   - +-inf (or anything beyond +-1e30) in l/u means "no bound", as in OSQP;
+ *   - a handle is not thread-safe.
+ *   - status codes are OSQP 0.6's status_val (MPCQP_SOLVED == 1, ...), strings via
+ *     mpcqp_status_string().
+ */
+#ifndef MPCQP_H
+#define MPCQP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCQP_OK 0
+#define MPCQP_E_INVALID (-1)      /* bad argument / dimension / pattern */
+#define MPCQP_E_HIP (-2)          /* HIP runtime failure */
+#define MPCQP_E_UNSUPPORTED (-3)  /* structure or setting this build cannot handle */
+#define MPCQP_E_NODATA (-4)       /* solve before set_data */
+
+/* OSQP 0.6 status_val values */
+#define MPCQP_SOLVED 1
+#define MPCQP_SOLVED_INACCURATE 2
+#define MPCQP_PRIMAL_INFEASIBLE_INACCURATE 3
+#define MPCQP_DUAL_INFEASIBLE_INACCURATE 4
+#define MPCQP_MAX_ITER_REACHED (-2)
+#define MPCQP_PRIMAL_INFEASIBLE (-3)
+#define MPCQP_DUAL_INFEASIBLE (-4)
+#define MPCQP_NON_CVX (-7)
+#define MPCQP_UNSOLVED (-10)
+
+typedef struct mpcqp_handle mpcqp_handle;
+
+/* Shared sparsity: P upper-triangular CSC (n x n), A CSC (m x n), sorted row indices. */
+typedef struct {
+  int32_t n, m;
+  const int32_t *Pp, *Pi; /* host, n+1 / nnz(P) */
+  const int32_t *Ap, *Ai; /* host, n+1 / nnz(A) */
+} mpcqp_structure;
+
+/* OSQP 0.6 settings (same names, meaning and defaults; see mpcqp_default_settings). */
+typedef struct {
+  double rho, sigma, alpha;
+  double eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
+  double delta, adaptive_rho_tolerance;
+  int32_t max_iter, scaling, adaptive_rho, adaptive_rho_interval;
+  int32_t polish, polish_refine_iter, check_termination, warm_start, scaled_termination;
+} mpcqp_settings;
+
+/* Per-instance solve information written by mpcqp_solve (device pointers, may be NULL). */
+typedef struct {
+  int32_t *status;      /* [B] OSQP status_val */
+  int32_t *iter;        /* [B] ADMM iterations */
+  int32_t *rho_updates; /* [B] adaptive-rho refactorizations */
+  double *obj_val;      /* [B] */
+  double *pri_res;      /* [B] */
+  double *dua_res;      /* [B] */
+  double *rho;          /* [B] rho after the solve (carried into the next solve, as OSQP) */
+} mpcqp_info;
+
+int mpcqp_default_settings(mpcqp_settings *s);
+
+/* Symbolic analysis (ordering, elimination tree, level schedules) + device allocation for a
+ * batch of `batch` instances.  `stream` is a hipStream_t (NULL = default stream). */
+int mpcqp_create(const mpcqp_structure *st, const mpcqp_settings *s, int32_t batch, void *stream,
+                 mpcqp_handle **out);
+int mpcqp_destroy(mpcqp_handle *h);
+
+/* Problem data (device): Px [nnzP] and q [n] shared by all instances; Ax [B*nnzA] (CSC order),
+ * l, u [B*m].  Resets the warm-start state of every instance (cold start, rho = settings.rho). */
+int mpcqp_set_data(mpcqp_handle *h, const double *Px, const double *q, const double *Ax,
+                   const double *l, const double *u);
+/* New bounds for every instance [B*m] (device). */
+int mpcqp_update_bounds(mpcqp_handle *h, const double *l, const double *u);
+/* New A values for every instance [B*nnzA] (device, CSC order). */
+int mpcqp_update_A(mpcqp_handle *h, const double *Ax);
+/* New shared linear cost q [n] (device). */
+int mpcqp_update_lin_cost(mpcqp_handle *h, const double *q);
+/* Warm start every instance from unscaled primal/dual guesses x [B*n], y [B*m] (device). */
+int mpcqp_warm_start(mpcqp_handle *h, const double *x, const double *y);
+
+/* Solve every instance (warm-started from its previous solve when settings.warm_start).
+ * x [B*n], y [B*m] device outputs (unscaled, NaN when no solution exists, as OSQP). */
+int mpcqp_solve(mpcqp_handle *h, double *x, double *y, const mpcqp_info *info);
+
+/* Introspection. */
+int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA,
+               int32_t *nnzL);
+/* Schedule statistics: number of level-scheduled steps of the factorization / forward / backward
+ * triangular solves, LDS bytes per instance and resident waves (instances in flight) per CU. */
+int mpcqp_schedule_info(const mpcqp_handle *h, int32_t *fac_steps, int32_t *fwd_steps,
+                        int32_t *bwd_steps, int32_t *lds_bytes, int32_t *waves_per_cu);
+/* Host-side export of the symbolic analysis for white-box tests (no device work):
+ * perm [n+m] (KKT position -> original KKT index), Lp [n+m+1], Li [nnzL]. */
+int mpcqp_export_symbolic(const mpcqp_handle *h, int32_t *perm, int32_t *Lp, int32_t *Li);
+const char *mpcqp_status_string(int32_t status);
+const char *mpcqp_last_error(void);
+/* ABI version (major*100 + minor). */
+int mpcqp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,113 @@
+"""ctypes binding of libmpcqp.so (the C ABI declared in include/mpcqp.h).
+
+The library is built in-tree by `__graft_entry__.build()` (hipcc --offload-arch=gfx950).  There is
+no fallback: if the shared object is missing, or no GPU is visible when a device call is made, the
+calls raise `MPCQPError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpcqp.so")
+
+# every symbol include/mpcqp.h declares (checked by tests/test_abi.py)
+EXPORTED = (
+    "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",
+    "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
+    "mpcqp_solve", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_export_symbolic",
+    "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version",
+)
+
+STATUS = {
+    1: "solved", 2: "solved inaccurate", 3: "primal infeasible inaccurate",
+    4: "dual infeasible inaccurate", -2: "maximum iterations reached", -3: "primal infeasible",
+    -4: "dual infeasible", -5: "interrupted", -6: "run time limit reached",
+    -7: "problem non convex", -10: "unsolved",
+}
+
+
+class MPCQPError(RuntimeError):
+    pass
+
+
+class Structure(C.Structure):
+    _fields_ = [("n", C.c_int32), ("m", C.c_int32),
+                ("Pp", C.POINTER(C.c_int32)), ("Pi", C.POINTER(C.c_int32)),
+                ("Ap", C.POINTER(C.c_int32)), ("Ai", C.POINTER(C.c_int32))]
+
+
+class Settings(C.Structure):
+    _fields_ = [
+        ("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double),
+        ("eps_abs", C.c_double), ("eps_rel", C.c_double),
+        ("eps_prim_inf", C.c_double), ("eps_dual_inf", C.c_double),
+        ("delta", C.c_double), ("adaptive_rho_tolerance", C.c_double),
+        ("max_iter", C.c_int32), ("scaling", C.c_int32), ("adaptive_rho", C.c_int32),
+        ("adaptive_rho_interval", C.c_int32), ("polish", C.c_int32),
+        ("polish_refine_iter", C.c_int32), ("check_termination", C.c_int32),
+        ("warm_start", C.c_int32), ("scaled_termination", C.c_int32),
+    ]
+
+
+class Info(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("iter", C.c_void_p), ("rho_updates", C.c_void_p),
+                ("obj_val", C.c_void_p), ("pri_res", C.c_void_p), ("dua_res", C.c_void_p),
+                ("rho", C.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libmpcqp.so (raises MPCQPError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MPCQPError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i32p, dp = C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.c_void_p
+    L.mpcqp_default_settings.argtypes = [C.POINTER(Settings)]
+    L.mpcqp_create.argtypes = [C.POINTER(Structure), C.POINTER(Settings), i32, vp,
+                               C.POINTER(vp)]
+    L.mpcqp_destroy.argtypes = [vp]
+    L.mpcqp_set_data.argtypes = [vp, dp, dp, dp, dp, dp]
+    L.mpcqp_update_bounds.argtypes = [vp, dp, dp]
+    L.mpcqp_update_A.argtypes = [vp, dp]
+    L.mpcqp_update_lin_cost.argtypes = [vp, dp]
+    L.mpcqp_warm_start.argtypes = [vp, dp, dp]
+    L.mpcqp_solve.argtypes = [vp, dp, dp, C.POINTER(Info)]
+    L.mpcqp_dims.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
+    L.mpcqp_schedule_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
+    L.mpcqp_export_symbolic.argtypes = [vp, i32p, i32p, i32p]
+    L.mpcqp_status_string.argtypes = [i32]
+    L.mpcqp_status_string.restype = C.c_char_p
+    L.mpcqp_last_error.restype = C.c_char_p
+    for name in EXPORTED:
+        fn = getattr(L, name)
+        if name not in ("mpcqp_status_string", "mpcqp_last_error"):
+            fn.restype = C.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().mpcqp_last_error().decode(errors="replace")
+        raise MPCQPError(f"{what} failed ({rc}): {msg}")
+
+
+def default_settings(**overrides) -> Settings:
+    s = Settings()
+    lib().mpcqp_default_settings(C.byref(s))
+    for k, v in overrides.items():
+        if k == "verbose":
+            continue
+        if k == "warm_starting":  # OSQP 1.x spelling
+            k = "warm_start"
+        if not any(k == f[0] for f in Settings._fields_):
+            raise ValueError(f"unknown setting '{k}'")
+        setattr(s, k, type(getattr(s, k))(v))
+    return s

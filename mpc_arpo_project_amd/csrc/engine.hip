@@ -1,0 +1,1379 @@
+// engine.hip -- MI355X (gfx950) batched OSQP-semantics QP engine: device kernel + C ABI.
+//
+// Design (DESIGN.md has the long form):
+//   * one QP instance per wavefront (64 lanes, one wave per workgroup), persistent grid sized to
+//     the resident-wave capacity; waves pull instance ids from an atomic work counter, so the
+//     heavy-tailed ADMM iteration counts balance themselves;
+//   * the instance's KKT factor L, 1/D and the solve vector live in LDS (16 KB at N = 20), the
+//     primal/dual iterates, bounds and scalings live in VGPRs (element i on lane i % 64, slot
+//     i / 64); scaled P/A values are parked in a per-wave scratch slab that stays L2-resident;
+//   * numeric factorization and both triangular solves are driven by host-compiled level
+//     schedules (symbolic.hpp): each step is a 64-lane dot-product/butterfly pass over LDS;
+//   * arithmetic is fp64 throughout and follows OSQP 0.6's algorithm (Ruiz scaling, rho classes,
+//     ADMM with alpha relaxation, unscaled termination + infeasibility tests, adaptive rho).
+//
+// Reference boundary replaced: osqp.OSQP setup/update/solve as called at
+// reference src/trajectorySimulate.py:242-348 (see include/mpcqp.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mpcqp.h"
+#include "symbolic.hpp"
+
+using namespace mpcqp;
+
+#define OSQP_INFTY 1e30
+#define RHO_MIN 1e-06
+#define RHO_MAX 1e06
+#define RHO_EQ_OVER_RHO_INEQ 1e03
+#define RHO_TOL 1e-04
+#define MIN_SCALING 1e-04
+#define MAX_SCALING 1e+04
+#define DIVISION_TOL 1e-30
+
+namespace {
+
+constexpr int MAXC = 8;  // terms per lane kept in the prefetch registers
+
+// ------------------------------------------------------------------------------------- device
+struct DevPlan {
+  const StepHdr *fac, *fwd, *bwd;
+  int nfac, nfwd, nbwd;
+  const uint32_t* meta;    // factorization pools (global)
+  const uint32_t* terms2;
+  const uint64_t* terms3;
+  const uint32_t* smeta;   // solve pools: global source of the per-workgroup LDS copy
+  const uint32_t* sterms;
+  int nsmeta, nsterms;     // words
+  int hdr_words;           // fwd + bwd + fac step headers, copied to the front of the table region
+  int tbl_words;           // LDS words of the table region (16-byte aligned)
+  int inst_doubles;        // LDS doubles per instance image (16-byte aligned)
+  const uint16_t *slotP, *slotA, *slotRho, *slotSig, *wsx, *wsz;
+  const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
+  int n, m, nk, nnzP, nnzA, nnzL;
+  int LX, DINV, W, ZERO, LDS_N, S_P, S_A, S_DT, S_ET;
+};
+
+struct KParams {
+  DevPlan pl;
+  mpcqp_settings s;
+  int B;
+  const double *Px, *q;      // shared
+  const double *Ax, *l, *u;  // [B][nnzA], [B][m]
+  // warm-start state carried between solves (OSQP keeps it inside the workspace)
+  double *xs, *zs, *ys, *rho_state, *Ecls;  // scaled iterates, rho, E of the previous scaling
+  int32_t* has_state;                        // 0 none, 1 scaled iterates, 2 unscaled guess
+  double *x_out, *y_out;
+  mpcqp_info info;
+  double* scratch;  // [grid][nnzP + nnzA] scaled P and A values of the wave's current instance
+  unsigned int* counter;
+};
+
+// Ordering between dependent wave-synchronous LDS phases.  A wave's LDS instructions are executed
+// in issue order, so a ds_read issued after a ds_write observes it; only the compiler has to be
+// stopped from reordering the memory operations (no hardware wait is needed).
+#define LDS_FENCE() asm volatile("" ::: "memory")
+
+__device__ __forceinline__ double dmaxd(double a, double b) { return a > b ? a : b; }
+__device__ __forceinline__ double dmind(double a, double b) { return a < b ? a : b; }
+
+// xor-butterfly reductions: every lane ends with the bitwise-identical result (each stage adds
+// the same two operands in both partner lanes; fp addition is commutative)
+__device__ __forceinline__ double wave_max(double x) {
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) x = dmaxd(x, __shfl_xor(x, k));
+  return x;
+}
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) x += __shfl_xor(x, k);
+  return x;
+}
+__device__ __forceinline__ double limit_scaling(double d) {
+  d = d < MIN_SCALING ? 1.0 : d;
+  return d > MAX_SCALING ? MAX_SCALING : d;
+}
+
+// ---- level-scheduled dot-product steps (see symbolic.hpp) ---------------------------------
+// Step headers live in the workgroup's LDS table region (copied at kernel start).
+__device__ __forceinline__ StepHdr ld_hdr(const StepHdr* p, int s) { return p[s]; }
+
+// 64-bit cross-lane moves for the group butterflies: DPP inside rows of 16 lanes (quad_perm xor 1,
+// xor 2, row_half_mirror, row_mirror pair the partners of an aligned group exactly like an xor
+// butterfly does for an all-reduce), ds_bpermute beyond that.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double group_partner(double x, int k) {
+  switch (k) {
+    case 0: return dpp_d<0xB1>(x);   // quad_perm [1,0,3,2]
+    case 1: return dpp_d<0x4E>(x);   // quad_perm [2,3,0,1]
+    case 2: return dpp_d<0x141>(x);  // row_half_mirror
+    case 3: return dpp_d<0x140>(x);  // row_mirror
+    default: return __shfl_xor(x, 1 << k);
+  }
+}
+// all-reduce of acc over this lane's aligned group of 2^gl lanes (glog = max over the step)
+__device__ __forceinline__ double group_sum(double acc, int glog, int gl) {
+  for (int k = 0; k < glog; ++k) {
+    const double o = group_partner(acc, k);
+    if (k < gl) acc += o;
+  }
+  return acc;
+}
+
+// straight-line dot products (two accumulators to halve the dependent FMA chain)
+// All 2C LDS reads are forced in front of the FMAs (sched_group_barrier: 0x100 = DS read,
+// 0x002 = VALU) so that they overlap instead of paying one LDS round trip per term.
+template <int C>
+__device__ __forceinline__ double dot2(const double* v, const uint32_t* t) {
+  double x[C], y[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    x[c] = v[t[c] & 0xffffu];
+    y[c] = v[t[c] >> 16];
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * C, 0);
+  __builtin_amdgcn_sched_group_barrier(0x002, 2 * C, 0);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    if (c & 1)
+      a1 = fma(x[c], y[c], a1);
+    else
+      a0 = fma(x[c], y[c], a0);
+  }
+  return a0 + a1;
+}
+template <int C>
+__device__ __forceinline__ double dot3(const double* v, const uint64_t* t) {
+  double x[C], y[C], d[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    x[c] = v[t[c] & 0xffffu];
+    y[c] = v[(t[c] >> 16) & 0xffffu];
+    d[c] = v[t[c] >> 32];
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 3 * C, 0);
+  __builtin_amdgcn_sched_group_barrier(0x002, 3 * C, 0);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    if (c & 1)
+      a1 = fma(x[c] * y[c], d[c], a1);
+    else
+      a0 = fma(x[c] * y[c], d[c], a0);
+  }
+  return a0 + a1;
+}
+
+struct Pref2 {
+  uint32_t mt;
+  uint32_t t[MAXC];
+};
+
+// branch-free fetch of one solve step's lane records from the workgroup's LDS tables: lanes past
+// cnt and terms past C read a clamped (valid) address and are replaced by the dummy record
+__device__ __forceinline__ void load2(const StepHdr& h, const uint32_t* tmeta,
+                                      const uint32_t* tterm, int lane, uint32_t dummy, Pref2& r) {
+  const int C = (int)(h.cfg & 0xffu), cnt = (int)h.cnt;
+  const bool in = lane < cnt;
+  const int li = in ? lane : 0;
+  const uint32_t mt = tmeta[h.off_meta + li];
+  r.mt = in ? mt : 0u;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int cc = c < C ? c : 0;
+    const uint32_t t = tterm[h.off_terms + cc * cnt + li];
+    r.t[c] = (in && c < C) ? t : dummy;
+  }
+}
+
+// forward / backward triangular solve: v[t] <- v[t] - sum_c v[a_c] * v[b_c]
+__device__ __forceinline__ void run_dot2(const KParams& p, const StepHdr* hdr, int nsteps,
+                                         const uint32_t* tmeta, const uint32_t* tterm, double* v,
+                                         int lane) {
+  if (nsteps <= 0) return;
+  const uint32_t dummy = (uint32_t)p.pl.ZERO | ((uint32_t)p.pl.ZERO << 16);
+  Pref2 cur, nxt;
+  StepHdr hc = ld_hdr(hdr, 0);
+  StepHdr hn = ld_hdr(hdr, nsteps > 1 ? 1 : 0);
+  load2(hc, tmeta, tterm, lane, dummy, cur);
+  for (int s = 0; s < nsteps; ++s) {
+    // records of step s+1 (header already in registers) and header of step s+2
+    load2(hn, tmeta, tterm, lane, dummy, nxt);
+    const StepHdr hn2 = ld_hdr(hdr, s + 2 < nsteps ? s + 2 : 0);
+    const int C = (int)(hc.cfg & 0xffu), glog = (int)((hc.cfg >> 8) & 0xffu);
+    double acc;
+    switch (C) {
+      case 0: acc = 0.0; break;
+      case 1: acc = dot2<1>(v, cur.t); break;
+      case 2: acc = dot2<2>(v, cur.t); break;
+      case 3: acc = dot2<3>(v, cur.t); break;
+      case 4: acc = dot2<4>(v, cur.t); break;
+      case 5: acc = dot2<5>(v, cur.t); break;
+      case 6: acc = dot2<6>(v, cur.t); break;
+      case 7: acc = dot2<7>(v, cur.t); break;
+      default: {
+        acc = dot2<8>(v, cur.t);
+        const int cnt = (int)hc.cnt, li = lane < cnt ? lane : 0;
+        for (int c = MAXC; c < C; ++c) {  // very long rows only
+          const uint32_t t = lane < cnt ? tterm[hc.off_terms + c * cnt + li] : dummy;
+          acc = fma(v[t & 0xffffu], v[t >> 16], acc);
+        }
+      }
+    }
+    acc = group_sum(acc, glog, (int)((cur.mt >> META_GLOG_SHIFT) & 7u));
+    if (cur.mt & META_HEAD) {
+      const int t = (int)(cur.mt & META_TGT_MASK);
+      v[t] = v[t] - acc;
+    }
+    LDS_FENCE();
+    cur = nxt;
+    hc = hn;
+    hn = hn2;
+  }
+}
+
+// numeric LDL' factorization (left-looking, dot-product form) + per-level scaling L_ij *= 1/D_j.
+// Records come from global memory (L2-resident); the next step's records are fetched while the
+// current step computes.
+constexpr int MAXC3 = 4;
+struct Pref3 {
+  uint32_t mt;
+  uint64_t t[MAXC3];
+};
+
+__device__ __forceinline__ void load3(const DevPlan& P, const StepHdr& h, int lane, uint64_t dummy,
+                                      Pref3& r) {
+  const int kind = (int)(h.cfg >> 16), C = (int)(h.cfg & 0xffu), cnt = (int)h.cnt;
+  const bool in = lane < cnt;
+  const int li = in ? lane : 0;
+  if (kind == KIND_SCALE) {
+    const uint32_t e = P.terms2[h.off_terms + li];
+    r.mt = in ? e : 0u;
+#pragma unroll
+    for (int c = 0; c < MAXC3; ++c) r.t[c] = dummy;
+  } else {
+    const uint32_t mt = P.meta[h.off_meta + li];
+    r.mt = in ? mt : 0u;
+#pragma unroll
+    for (int c = 0; c < MAXC3; ++c) {
+      const int cc = c < C ? c : 0;
+      const uint64_t t = P.terms3[h.off_terms + (size_t)cc * cnt + li];
+      r.t[c] = (in && c < C) ? t : dummy;
+    }
+  }
+}
+
+__device__ __forceinline__ void run_factor(const KParams& p, double* v, int lane) {
+  const DevPlan& P = p.pl;
+  if (P.nfac <= 0) return;
+  const uint64_t dummy3 = (uint64_t)P.ZERO | ((uint64_t)P.ZERO << 16) | ((uint64_t)P.ZERO << 32);
+  Pref3 cur, nxt;
+  StepHdr hc = ld_hdr(P.fac, 0);
+  load3(P, hc, lane, dummy3, cur);
+  for (int s = 0; s < P.nfac; ++s) {
+    const StepHdr hn = ld_hdr(P.fac, s + 1 < P.nfac ? s + 1 : 0);
+    load3(P, hn, lane, dummy3, nxt);
+    const int kind = (int)(hc.cfg >> 16), C = (int)(hc.cfg & 0xffu);
+    if (kind == KIND_SCALE) {
+      if (lane < (int)hc.cnt) {
+        const int a = (int)(cur.mt & 0xffffu), d = (int)(cur.mt >> 16);
+        v[a] = v[a] * v[d];
+      }
+    } else {
+      double acc;
+      switch (C) {
+        case 0: acc = 0.0; break;
+        case 1: acc = dot3<1>(v, cur.t); break;
+        case 2: acc = dot3<2>(v, cur.t); break;
+        case 3: acc = dot3<3>(v, cur.t); break;
+        default: {
+          acc = dot3<4>(v, cur.t);
+          const int cnt = (int)hc.cnt, li = lane < cnt ? lane : 0;
+          for (int c = MAXC3; c < C; ++c) {
+            const uint64_t t =
+                lane < cnt ? P.terms3[hc.off_terms + (size_t)c * cnt + li] : dummy3;
+            acc = fma(v[t & 0xffffu] * v[(t >> 16) & 0xffffu], v[t >> 32], acc);
+          }
+        }
+      }
+      acc = group_sum(acc, (int)((hc.cfg >> 8) & 0xffu), (int)((cur.mt >> META_GLOG_SHIFT) & 7u));
+      if (cur.mt & META_HEAD) {
+        const int t = (int)(cur.mt & META_TGT_MASK);
+        const double nv = v[t] - acc;
+        v[t] = nv;
+        if (cur.mt & META_ISD) v[P.DINV + (t - P.W)] = 1.0 / nv;
+      }
+    }
+    LDS_FENCE();
+    cur = nxt;
+    hc = hn;
+  }
+}
+
+// constraint classes packed 2 bits per register slot (auxil.c constr_type)
+enum : uint32_t { CT_INEQ = 0, CT_EQ = 1, CT_FREE = 2 };
+
+// Register-resident per-instance state.  Element i of an n- or m-vector lives on lane i % 64,
+// slot i / 64.  Scalings D, 1/D, E, 1/E live in the wave's scratch slab (read at checks only).
+template <int RN, int RM>
+struct Inst {
+  double x[RN], q[RN];
+  double z[RM], y[RM], l[RM], u[RM];
+  uint32_t ct;  // 2 bits per slot
+  double rinv[RM], rvec[RM];  // rho_inv_vec / rho_vec of the lane's rows
+  double c, cinv, rho;
+  double rv_eq, ri_eq, ri_in, ri_free;  // rho_vec / rho_inv_vec values per class
+  double pri_res, dua_res;
+};
+
+// per-wave scratch slab layout (doubles)
+struct Slab {
+  double *Ps, *As, *D, *Dinv, *E, *Einv;
+};
+__device__ __forceinline__ Slab slab_of(const DevPlan& P, double* scr) {
+  Slab s;
+  s.Ps = scr;
+  s.As = s.Ps + P.nnzP;
+  s.D = s.As + P.nnzA;
+  s.Dinv = s.D + P.n;
+  s.E = s.Dinv + P.n;
+  s.Einv = s.E + P.m;
+  return s;
+}
+
+template <int RN, int RM>
+__device__ __forceinline__ uint32_t ctype(const Inst<RN, RM>& S, int r) {
+  return (S.ct >> (2 * r)) & 3u;
+}
+template <int RN, int RM>
+__device__ __forceinline__ double rinv_of(const Inst<RN, RM>& S, int r) {
+  return S.rinv[r];
+}
+template <int RN, int RM>
+__device__ __forceinline__ double rvec_of(const Inst<RN, RM>& S, int r) {
+  return S.rvec[r];
+}
+// rho_vec / rho_inv_vec values, computed exactly as OSQP computes them
+// (auxil.c set_rho_vec, osqp.c osqp_update_rho): rho_inv = 1 / rho_vec elementwise.
+template <int RN, int RM>
+__device__ __forceinline__ void set_rho(Inst<RN, RM>& S) {
+  S.rv_eq = RHO_EQ_OVER_RHO_INEQ * S.rho;
+  S.ri_eq = 1. / S.rv_eq;
+  S.ri_in = 1. / S.rho;
+  S.ri_free = 1. / RHO_MIN;
+  // per-row values by explicit predicated moves (a `?:` chain here is turned into a
+  // scratch-memory lookup table by the compiler)
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const uint32_t t = ctype(S, r);
+    double ri = S.ri_in, rv = S.rho;
+    if (t == CT_EQ) ri = S.ri_eq, rv = S.rv_eq;
+    if (t == CT_FREE) ri = S.ri_free, rv = RHO_MIN;
+    S.rinv[r] = ri;
+    S.rvec[r] = rv;
+  }
+}
+
+template <int RN, int RM>
+struct Resid {
+  double Ax[RM], Px[RN], Aty[RN];
+};
+
+// KKT values [[P + sigma I, A'], [A, -diag(1/rho)]] into the permuted LDS image
+// (OSQP kkt.c form_KKT / update_KKT_*), then factorize.
+template <int RN, int RM>
+__device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab& sb, double* v, int lane,
+                                    const Inst<RN, RM>& S) {
+  const DevPlan& P = p.pl;
+  for (int k = lane; k < P.nnzL; k += 64) v[P.LX + k] = 0.0;
+  for (int k = lane; k < P.nk; k += 64) v[P.W + k] = 0.0;
+  if (lane == 0) v[P.ZERO] = 0.0;
+  LDS_FENCE();
+  for (int j = lane; j < P.n; j += 64) v[P.slotSig[j]] = p.s.sigma;
+  LDS_FENCE();
+  for (int k = lane; k < P.nnzP; k += 64) {
+    const double val = sb.Ps[k];
+    v[P.slotP[k]] = (P.Pi[k] == P.Pcol[k]) ? val + p.s.sigma : val;
+  }
+  for (int k = lane; k < P.nnzA; k += 64) v[P.slotA[k]] = sb.As[k];
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    if (i < P.m) v[P.slotRho[i]] = -rinv_of(S, r);
+  }
+  LDS_FENCE();
+  run_factor(p, v, lane);
+}
+
+// update_info: scaled Ax, Px, A'y and the unscaled residual norms (auxil.c compute_pri_res /
+// compute_dua_res).  x and y are staged as plain arrays in the W region.
+template <int RN, int RM>
+__device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>& S, Resid<RN, RM>& R,
+                                  const Slab& sb, double* v, int lane) {
+  const DevPlan& P = p.pl;
+  const int n = P.n, m = P.m;
+  double* xb = v + P.W;
+  double* yb = v + P.W + n;
+  LDS_FENCE();
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int i = lane + 64 * r;
+    if (i < n) xb[i] = S.x[r];
+  }
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    if (i < m) yb[i] = S.y[r];
+  }
+  LDS_FENCE();
+  double pr = 0.0, dr = 0.0;
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    double s = 0.0;
+    if (i < m) {
+      for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) s += sb.As[P.Ark[q]] * xb[P.Arj[q]];
+      pr = dmaxd(pr, fabs(sb.Einv[i] * (s - S.z[r])));
+    }
+    R.Ax[r] = s;
+  }
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    double sp = 0.0, sa = 0.0;
+    if (j < n) {
+      for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) sp += sb.Ps[P.Psk[e]] * xb[P.Pso[e]];
+      for (int k = P.Ap[j]; k < P.Ap[j + 1]; ++k) sa += sb.As[k] * yb[P.Ai[k]];
+      dr = dmaxd(dr, fabs(sb.Dinv[j] * ((S.q[r] + sp) + sa)));
+    }
+    R.Px[r] = sp;
+    R.Aty[r] = sa;
+  }
+  S.pri_res = wave_max(pr);
+  S.dua_res = S.cinv * wave_max(dr);
+}
+
+template <int RN, int RM>
+__device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, RM>& S, double (&dy)[RM],
+                                     const Slab& sb, double* v, int lane, double eps) {
+  const DevPlan& P = p.pl;
+  const double thr = OSQP_INFTY * MIN_SCALING;
+  double nrm = 0.0;
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    if (i < P.m) {
+      if (S.u[r] > thr)
+        dy[r] = (S.l[r] < -thr) ? 0.0 : dmind(dy[r], 0.0);
+      else if (S.l[r] < -thr)
+        dy[r] = dmaxd(dy[r], 0.0);
+      nrm = dmaxd(nrm, fabs(sb.E[i] * dy[r]));
+    }
+  }
+  nrm = wave_max(nrm);
+  if (!(nrm > DIVISION_TOL)) return false;
+  double lhs = 0.0;
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    if (i < P.m) lhs += S.u[r] * dmaxd(dy[r], 0.0) + S.l[r] * dmind(dy[r], 0.0);
+  }
+  lhs = wave_sum(lhs);
+  if (!(lhs < eps * nrm)) return false;
+  double* yb = v + P.W + P.n;
+  LDS_FENCE();
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    if (i < P.m) yb[i] = dy[r];
+  }
+  LDS_FENCE();
+  double mx = 0.0;
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    if (j < P.n) {
+      double s = 0.0;
+      for (int k = P.Ap[j]; k < P.Ap[j + 1]; ++k) s += sb.As[k] * yb[P.Ai[k]];
+      mx = dmaxd(mx, fabs(s * sb.Dinv[j]));
+    }
+  }
+  mx = wave_max(mx);
+  return mx < eps * nrm;
+}
+
+template <int RN, int RM>
+__device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM>& S, const double (&dx)[RN],
+                                   const Slab& sb, double* v, int lane, double eps) {
+  const DevPlan& P = p.pl;
+  const double thr = OSQP_INFTY * MIN_SCALING;
+  double nrm = 0.0, qdx = 0.0;
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    if (j < P.n) {
+      nrm = dmaxd(nrm, fabs(sb.D[j] * dx[r]));
+      qdx += S.q[r] * dx[r];
+    }
+  }
+  nrm = wave_max(nrm);
+  if (!(nrm > DIVISION_TOL)) return false;
+  qdx = wave_sum(qdx);
+  if (!(qdx < S.c * eps * nrm)) return false;
+  double* xb = v + P.W;
+  LDS_FENCE();
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    if (j < P.n) xb[j] = dx[r];
+  }
+  LDS_FENCE();
+  double mx = 0.0;
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    if (j < P.n) {
+      double s = 0.0;
+      for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) s += sb.Ps[P.Psk[e]] * xb[P.Pso[e]];
+      mx = dmaxd(mx, fabs(s * sb.Dinv[j]));
+    }
+  }
+  mx = wave_max(mx);
+  if (!(mx < S.c * eps * nrm)) return false;
+  int bad = 0;
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    if (i < P.m) {
+      double s = 0.0;
+      for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) s += sb.As[P.Ark[q]] * xb[P.Arj[q]];
+      s *= sb.Einv[i];
+      if ((S.u[r] < thr && s > eps * nrm) || (S.l[r] > -thr && s < -eps * nrm)) bad = 1;
+    }
+  }
+  return !__any(bad);
+}
+
+template <int RN, int RM>
+__device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>& S, const Resid<RN, RM>& R,
+                                 double (&dy)[RM], const double (&dx)[RN], const Slab& sb,
+                                 double* v, int lane, bool approximate) {
+  const DevPlan& P = p.pl;
+  double eps_abs = p.s.eps_abs, eps_rel = p.s.eps_rel;
+  double eps_pinf = p.s.eps_prim_inf, eps_dinf = p.s.eps_dual_inf;
+  if (approximate) eps_abs *= 10, eps_rel *= 10, eps_pinf *= 10, eps_dinf *= 10;
+  // compute_pri_tol / compute_dua_tol (unscaled termination)
+  double zn = 0.0, axn = 0.0, qn = 0.0, atn = 0.0, pxn = 0.0;
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    if (i < P.m) {
+      const double ei = sb.Einv[i];
+      zn = dmaxd(zn, fabs(ei * S.z[r]));
+      axn = dmaxd(axn, fabs(ei * R.Ax[r]));
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    if (j < P.n) {
+      const double di = sb.Dinv[j];
+      qn = dmaxd(qn, fabs(di * S.q[r]));
+      atn = dmaxd(atn, fabs(di * R.Aty[r]));
+      pxn = dmaxd(pxn, fabs(di * R.Px[r]));
+    }
+  }
+  zn = wave_max(zn), axn = wave_max(axn), qn = wave_max(qn), atn = wave_max(atn);
+  pxn = wave_max(pxn);
+  const double eps_prim = eps_abs + eps_rel * dmaxd(zn, axn);
+  const double eps_dual = eps_abs + eps_rel * (dmaxd(dmaxd(qn, atn), pxn) * S.cinv);
+  bool prim_ok = false, dual_ok = false, prim_inf = false, dual_inf = false;
+  if (S.pri_res < eps_prim)
+    prim_ok = true;
+  else
+    prim_inf = is_primal_infeasible(p, S, dy, sb, v, lane, eps_pinf);
+  if (S.dua_res < eps_dual)
+    dual_ok = true;
+  else
+    dual_inf = is_dual_infeasible(p, S, dx, sb, v, lane, eps_dinf);
+  if (prim_ok && dual_ok) return approximate ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED;
+  if (prim_inf) return approximate ? MPCQP_PRIMAL_INFEASIBLE_INACCURATE : MPCQP_PRIMAL_INFEASIBLE;
+  if (dual_inf) return approximate ? MPCQP_DUAL_INFEASIBLE_INACCURATE : MPCQP_DUAL_INFEASIBLE;
+  return 0;
+}
+
+// auxil.c compute_rho_estimate (residual vectors in scaled space)
+template <int RN, int RM>
+__device__ __forceinline__ double rho_estimate(const KParams& p, const Inst<RN, RM>& S, const Resid<RN, RM>& R,
+                               int lane) {
+  const DevPlan& P = p.pl;
+  double pr = 0.0, zn = 0.0, axn = 0.0, dr = 0.0, qn = 0.0, atn = 0.0, pxn = 0.0;
+#pragma unroll
+  for (int r = 0; r < RM; ++r)
+    if (lane + 64 * r < P.m) {
+      pr = dmaxd(pr, fabs(R.Ax[r] - S.z[r]));
+      zn = dmaxd(zn, fabs(S.z[r]));
+      axn = dmaxd(axn, fabs(R.Ax[r]));
+    }
+#pragma unroll
+  for (int r = 0; r < RN; ++r)
+    if (lane + 64 * r < P.n) {
+      dr = dmaxd(dr, fabs((S.q[r] + R.Px[r]) + R.Aty[r]));
+      qn = dmaxd(qn, fabs(S.q[r]));
+      atn = dmaxd(atn, fabs(R.Aty[r]));
+      pxn = dmaxd(pxn, fabs(R.Px[r]));
+    }
+  pr = wave_max(pr), zn = wave_max(zn), axn = wave_max(axn);
+  dr = wave_max(dr), qn = wave_max(qn), atn = wave_max(atn), pxn = wave_max(pxn);
+  pr /= (dmaxd(zn, axn) + DIVISION_TOL);
+  dr /= (dmaxd(dmaxd(qn, atn), pxn) + DIVISION_TOL);
+  double est = S.rho * sqrt(pr / (dr + DIVISION_TOL));
+  return dmind(dmaxd(est, RHO_MIN), RHO_MAX);
+}
+
+__device__ __forceinline__ bool has_solution(int st) {
+  return st != MPCQP_PRIMAL_INFEASIBLE && st != MPCQP_PRIMAL_INFEASIBLE_INACCURATE &&
+         st != MPCQP_DUAL_INFEASIBLE && st != MPCQP_DUAL_INFEASIBLE_INACCURATE &&
+         st != MPCQP_NON_CVX;
+}
+
+// Ruiz equilibration (scaling.c scale_data) of the instance's P (shared values) and A, q, l, u.
+// Leaves scaled P/A in the slab, D, 1/D, E, 1/E in the slab, and q, l, u (scaled) and the
+// constraint classes in registers.
+template <int RN, int RM>
+__device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs, Inst<RN, RM>& S, const Slab& sb,
+                              double* v, int lane) {
+  const DevPlan& P = p.pl;
+  const int n = P.n, m = P.m;
+  const double* Ax_in = p.Ax + (size_t)inst * P.nnzA;
+  const double* l_in = p.l + (size_t)inst * m;
+  const double* u_in = p.u + (size_t)inst * m;
+  double D[RN], E[RM];
+  for (int k = lane; k < P.nnzP; k += 64) v[P.S_P + k] = p.Px[k];
+  for (int k = lane; k < P.nnzA; k += 64) v[P.S_A + k] = Ax_in[k];
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    S.q[r] = j < n ? p.q[j] : 0.0;
+    D[r] = 1.0;
+  }
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    S.l[r] = i < m ? dmaxd(l_in[i], -OSQP_INFTY) : 0.0;
+    S.u[r] = i < m ? dmind(u_in[i], OSQP_INFTY) : 0.0;
+    E[r] = 1.0;
+  }
+  S.c = 1.0;
+  LDS_FENCE();
+  for (int it = 0; it < p.s.scaling; ++it) {
+    double dt[RN], et[RM];
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+      const int j = lane + 64 * r;
+      double d = 0.0;
+      if (j < n) {
+        for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) d = dmaxd(fabs(v[P.S_P + P.Psk[e]]), d);
+        double da = 0.0;
+        for (int k = P.Ap[j]; k < P.Ap[j + 1]; ++k) da = dmaxd(fabs(v[P.S_A + k]), da);
+        d = dmaxd(d, da);
+      }
+      d = sqrt(limit_scaling(d));
+      dt[r] = 1. / d;
+      if (j < n) v[P.S_DT + j] = dt[r];
+    }
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int i = lane + 64 * r;
+      double e = 0.0;
+      if (i < m)
+        for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) e = dmaxd(fabs(v[P.S_A + P.Ark[q]]), e);
+      e = sqrt(limit_scaling(e));
+      et[r] = 1. / e;
+      if (i < m) v[P.S_ET + i] = et[r];
+    }
+    LDS_FENCE();
+    for (int k = lane; k < P.nnzP; k += 64)
+      v[P.S_P + k] = (v[P.S_P + k] * v[P.S_DT + P.Pi[k]]) * v[P.S_DT + P.Pcol[k]];
+    for (int k = lane; k < P.nnzA; k += 64)
+      v[P.S_A + k] = (v[P.S_A + k] * v[P.S_ET + P.Ai[k]]) * v[P.S_DT + P.Acol[k]];
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+      S.q[r] = dt[r] * S.q[r];
+      D[r] = D[r] * dt[r];
+    }
+#pragma unroll
+    for (int r = 0; r < RM; ++r) E[r] = E[r] * et[r];
+    LDS_FENCE();
+    // cost normalization
+    double csum = 0.0, qmax = 0.0;
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+      const int j = lane + 64 * r;
+      if (j < n) {
+        double d = 0.0;
+        for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) d = dmaxd(fabs(v[P.S_P + P.Psk[e]]), d);
+        csum += d;
+        qmax = dmaxd(qmax, fabs(S.q[r]));
+      }
+    }
+    double c_temp = wave_sum(csum) / n;
+    const double inq = limit_scaling(wave_max(qmax));
+    c_temp = limit_scaling(dmaxd(c_temp, inq));
+    c_temp = 1. / c_temp;
+    for (int k = lane; k < P.nnzP; k += 64) v[P.S_P + k] = v[P.S_P + k] * c_temp;
+#pragma unroll
+    for (int r = 0; r < RN; ++r) S.q[r] = S.q[r] * c_temp;
+    S.c = S.c * c_temp;
+    LDS_FENCE();
+  }
+  S.cinv = 1. / S.c;
+  // constraint classes (auxil.c set_rho_vec / update_rho_vec): with warm state OSQP classifies
+  // on bounds scaled by the PREVIOUS equilibration (update_bounds precedes the rescale of
+  // update_A), on first use by the new one.
+  const double thr = OSQP_INFTY * MIN_SCALING;
+  const double* Eold = p.Ecls + (size_t)inst * m;
+  S.ct = 0;
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    const double ec = (hs == 1 && i < m) ? Eold[i] : E[r];
+    const double lc = S.l[r] * ec, uc = S.u[r] * ec;
+    const uint32_t t = (lc < -thr && uc > thr) ? CT_FREE : ((uc - lc < RHO_TOL) ? CT_EQ : CT_INEQ);
+    S.ct |= t << (2 * r);
+    S.l[r] = E[r] * S.l[r];
+    S.u[r] = E[r] * S.u[r];
+    if (i < m) {
+      sb.E[i] = E[r];
+      sb.Einv[i] = 1. / E[r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    if (j < n) {
+      sb.D[j] = D[r];
+      sb.Dinv[j] = 1. / D[r];
+    }
+  }
+  // park scaled P, A for residuals / refactorization (per-wave slab, L2-resident)
+  for (int k = lane; k < P.nnzP; k += 64) sb.Ps[k] = v[P.S_P + k];
+  for (int k = lane; k < P.nnzA; k += 64) sb.As[k] = v[P.S_A + k];
+  LDS_FENCE();
+}
+
+template <int RN, int RM>
+__device__ __forceinline__ void solve_instance(const KParams& p, int inst, double* v, double* scr,
+                                               const uint32_t* tmeta, const uint32_t* tterm,
+                                               int lane) {
+  const DevPlan& P = p.pl;
+  const int n = P.n, m = P.m;
+  const Slab sb = slab_of(P, scr);
+  Inst<RN, RM> S;
+  const int hs = p.has_state[inst];
+  scale_problem<RN, RM>(p, inst, hs, S, sb, v, lane);
+  S.rho = (hs != 0) ? p.rho_state[inst] : dmind(dmaxd(p.s.rho, RHO_MIN), RHO_MAX);
+  set_rho(S);
+  assemble_and_factor<RN, RM>(p, sb, v, lane, S);
+
+  // ---------------- warm start
+  const bool warm = p.s.warm_start && hs != 0;
+  if (warm && hs == 1) {
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+      const int j = lane + 64 * r;
+      S.x[r] = j < n ? p.xs[(size_t)inst * n + j] : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int i = lane + 64 * r;
+      S.z[r] = i < m ? p.zs[(size_t)inst * m + i] : 0.0;
+      S.y[r] = i < m ? p.ys[(size_t)inst * m + i] : 0.0;
+    }
+  } else if (warm && hs == 2) {  // osqp_warm_start: scale the user guess, z = A x
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+      const int j = lane + 64 * r;
+      S.x[r] = j < n ? sb.Dinv[j] * p.xs[(size_t)inst * n + j] : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int i = lane + 64 * r;
+      S.y[r] = i < m ? (sb.Einv[i] * p.ys[(size_t)inst * m + i]) * S.c : 0.0;
+    }
+    double* xb = v + P.W;
+    LDS_FENCE();
+#pragma unroll
+    for (int r = 0; r < RN; ++r)
+      if (lane + 64 * r < n) xb[lane + 64 * r] = S.x[r];
+    LDS_FENCE();
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int i = lane + 64 * r;
+      double s = 0.0;
+      if (i < m)
+        for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) s += sb.As[P.Ark[q]] * xb[P.Arj[q]];
+      S.z[r] = s;
+    }
+    LDS_FENCE();
+  } else {
+#pragma unroll
+    for (int r = 0; r < RN; ++r) S.x[r] = 0.0;
+#pragma unroll
+    for (int r = 0; r < RM; ++r) S.z[r] = 0.0, S.y[r] = 0.0;
+  }
+  S.pri_res = S.dua_res = 0.0;
+
+  // ---------------- ADMM (osqp.c osqp_solve)
+  // LDS slots of this lane's x / z entries in the permuted solve vector (kept in registers)
+  int wsx[RN], wsz[RM];
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    wsx[r] = j < n ? (int)P.wsx[j] : P.ZERO + 1;
+  }
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    wsz[r] = i < m ? (int)P.wsz[i] : P.ZERO + 1;
+  }
+  const double sigma = p.s.sigma, alpha = p.s.alpha;
+  const int chk = p.s.check_termination;
+  int ar_int = p.s.adaptive_rho_interval;
+  if (p.s.adaptive_rho && ar_int == 0) ar_int = chk ? 4 * chk : 100;
+  int status = MPCQP_UNSOLVED, iter = 0, rho_updates = 0;
+  bool can_check = false;
+  double dx[RN], dy[RM];
+  Resid<RN, RM> R;
+  for (iter = 1; iter <= p.s.max_iter; ++iter) {
+    double xp[RN], zp[RM], bz[RM];
+    // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+      const int j = lane + 64 * r;
+      xp[r] = S.x[r];
+      if (j < n) v[wsx[r]] = sigma * xp[r] - S.q[r];
+    }
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int i = lane + 64 * r;
+      zp[r] = S.z[r];
+      bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
+      if (i < m) v[wsz[r]] = bz[r];
+    }
+    LDS_FENCE();
+    run_dot2(p, P.fwd, P.nfwd, tmeta, tterm, v, lane);
+    for (int k = lane; k < P.nk; k += 64) v[P.W + k] = v[P.W + k] * v[P.DINV + k];
+    LDS_FENCE();
+    run_dot2(p, P.bwd, P.nbwd, tmeta, tterm, v, lane);
+    // x, z, y updates (auxil.c update_x / update_z / update_y)
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+      const int j = lane + 64 * r;
+      const double xt = j < n ? v[wsx[r]] : 0.0;
+      S.x[r] = alpha * xt + (1.0 - alpha) * xp[r];
+      dx[r] = S.x[r] - xp[r];
+    }
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int i = lane + 64 * r;
+      const double nu = i < m ? v[wsz[r]] : 0.0;
+      const double ri = rinv_of(S, r);
+      const double zt = bz[r] + ri * nu;
+      const double zr = alpha * zt + (1.0 - alpha) * zp[r];
+      S.z[r] = dmind(dmaxd(zr + ri * S.y[r], S.l[r]), S.u[r]);
+      dy[r] = rvec_of(S, r) * (zr - S.z[r]);
+      S.y[r] = S.y[r] + dy[r];
+    }
+    LDS_FENCE();
+    can_check = chk && (iter % chk == 0);
+    const bool adapt = p.s.adaptive_rho && ar_int && (iter % ar_int == 0);
+#ifndef EXP_NOCHECK
+    if (can_check || adapt) compute_residuals(p, S, R, sb, v, lane);
+#endif
+    if (can_check) {
+#ifdef EXP_NOCHECK
+      if (iter > 100) break;
+      continue;
+#endif
+      status = check_termination(p, S, R, dy, dx, sb, v, lane, false);
+      if (status != 0) break;
+      status = MPCQP_UNSOLVED;
+    }
+    if (adapt) {
+      const double rho_new = rho_estimate(p, S, R, lane);
+      if (rho_new > S.rho * p.s.adaptive_rho_tolerance ||
+          rho_new < S.rho / p.s.adaptive_rho_tolerance) {
+        S.rho = dmind(dmaxd(rho_new, RHO_MIN), RHO_MAX);
+        set_rho(S);
+        rho_updates++;
+        LDS_FENCE();
+        assemble_and_factor<RN, RM>(p, sb, v, lane, S);
+      }
+    }
+  }
+  if (!can_check) {
+    iter = iter - 1;
+    compute_residuals(p, S, R, sb, v, lane);
+    status = check_termination(p, S, R, dy, dx, sb, v, lane, false);
+    if (status == 0) status = MPCQP_UNSOLVED;
+  }
+  if (iter > p.s.max_iter) iter = p.s.max_iter;
+  if (status == MPCQP_UNSOLVED) {
+    const int st = check_termination(p, S, R, dy, dx, sb, v, lane, true);
+    status = st ? st : MPCQP_MAX_ITER_REACHED;
+  }
+
+  // ---------------- objective (compute_obj_val) and store_solution
+  const bool sol = has_solution(status);
+  double obj = 0.0;
+  if (sol) {
+    double* xb = v + P.W;
+    LDS_FENCE();
+#pragma unroll
+    for (int r = 0; r < RN; ++r)
+      if (lane + 64 * r < n) xb[lane + 64 * r] = S.x[r];
+    LDS_FENCE();
+    double part = 0.0;
+    for (int k = lane; k < P.nnzP; k += 64) {
+      const int i = P.Pi[k], j = P.Pcol[k];
+      part += (i == j) ? .5 * sb.Ps[k] * xb[i] * xb[i] : sb.Ps[k] * xb[i] * xb[j];
+    }
+#pragma unroll
+    for (int r = 0; r < RN; ++r)
+      if (lane + 64 * r < n) part += S.q[r] * S.x[r];
+    obj = wave_sum(part) * S.cinv;
+  } else if (status == MPCQP_PRIMAL_INFEASIBLE || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE) {
+    obj = OSQP_INFTY;
+  } else if (status == MPCQP_DUAL_INFEASIBLE || status == MPCQP_DUAL_INFEASIBLE_INACCURATE) {
+    obj = -OSQP_INFTY;
+  }
+  const double qnan = __builtin_nan("");
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    if (j < n) {
+      if (p.x_out) p.x_out[(size_t)inst * n + j] = sol ? sb.D[j] * S.x[r] : qnan;
+      p.xs[(size_t)inst * n + j] = sol ? S.x[r] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+    if (i < m) {
+      if (p.y_out) p.y_out[(size_t)inst * m + i] = sol ? (sb.E[i] * S.y[r]) * S.cinv : qnan;
+      p.zs[(size_t)inst * m + i] = sol ? S.z[r] : 0.0;
+      p.ys[(size_t)inst * m + i] = sol ? S.y[r] : 0.0;
+      p.Ecls[(size_t)inst * m + i] = sb.E[i];
+    }
+  }
+  if (lane == 0) {
+    p.rho_state[inst] = S.rho;
+    p.has_state[inst] = 1;
+    if (p.info.status) p.info.status[inst] = status;
+    if (p.info.iter) p.info.iter[inst] = iter;
+    if (p.info.rho_updates) p.info.rho_updates[inst] = rho_updates;
+    if (p.info.obj_val) p.info.obj_val[inst] = obj;
+    if (p.info.pri_res) p.info.pri_res[inst] = S.pri_res;
+    if (p.info.dua_res) p.info.dua_res[inst] = S.dua_res;
+    if (p.info.rho) p.info.rho[inst] = S.rho;
+  }
+}
+
+// One workgroup = WPG <= 8 waves (blockDim.x = 64 * WPG); each wave solves its own instances.  The
+// workgroup's LDS holds one copy of the solve schedules followed by one instance image per wave.
+template <int RN, int RM>
+__global__ void __launch_bounds__(512) qp_batch_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = (int)(threadIdx.x & 63);
+  const int wave = (int)(threadIdx.x >> 6);
+  const int wpg = (int)(blockDim.x >> 6);
+  uint32_t* tbl = reinterpret_cast<uint32_t*>(lds);
+  const uint32_t* hsrc[3] = {reinterpret_cast<const uint32_t*>(p.pl.fwd),
+                             reinterpret_cast<const uint32_t*>(p.pl.bwd),
+                             reinterpret_cast<const uint32_t*>(p.pl.fac)};
+  const int hn[3] = {4 * p.pl.nfwd, 4 * p.pl.nbwd, 4 * p.pl.nfac};
+  int off = 0;
+  for (int q = 0; q < 3; ++q) {
+    for (int k = (int)threadIdx.x; k < hn[q]; k += (int)blockDim.x) tbl[off + k] = hsrc[q][k];
+    off += hn[q];
+  }
+  for (int k = (int)threadIdx.x; k < p.pl.nsmeta; k += (int)blockDim.x)
+    tbl[p.pl.hdr_words + k] = p.pl.smeta[k];
+  for (int k = (int)threadIdx.x; k < p.pl.nsterms; k += (int)blockDim.x)
+    tbl[p.pl.hdr_words + p.pl.nsmeta + k] = p.pl.sterms[k];
+  __syncthreads();
+  KParams q = p;  // schedule headers now read from the workgroup's LDS copy
+  q.pl.fwd = reinterpret_cast<const StepHdr*>(tbl);
+  q.pl.bwd = q.pl.fwd + p.pl.nfwd;
+  q.pl.fac = q.pl.bwd + p.pl.nbwd;
+  const uint32_t* tmeta = tbl + p.pl.hdr_words;
+  const uint32_t* tterm = tmeta + p.pl.nsmeta;
+  double* v = lds + p.pl.tbl_words / 2 + (size_t)wave * p.pl.inst_doubles;
+  const size_t slab = (size_t)(p.pl.nnzP + p.pl.nnzA + 2 * p.pl.n + 2 * p.pl.m);
+  double* scr = p.scratch + ((size_t)blockIdx.x * wpg + wave) * slab;
+  for (;;) {
+    unsigned int inst = 0;
+    if (lane == 0) inst = atomicAdd(p.counter, 1u);
+    inst = (unsigned int)__shfl((int)inst, 0);
+    inst = __builtin_amdgcn_readfirstlane(inst);
+    if (inst >= (unsigned int)p.B) break;
+    solve_instance<RN, RM>(q, (int)inst, v, scr, tmeta, tterm, lane);
+    LDS_FENCE();
+  }
+}
+
+// ---------------------------------------------------------------------------------------- host
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) return fail(MPCQP_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+typedef void (*kernel_fn)(KParams);
+
+template <int RN, int RM>
+kernel_fn pick() {
+  return qp_batch_kernel<RN, RM>;
+}
+
+// RN = ceil(n/64) and RM = ceil(m/64) rounded up to the instantiated buckets
+kernel_fn select_kernel(int n, int m) {
+  const int rn = (n + 63) / 64, rm = (m + 63) / 64;
+  if (rn <= 2 && rm <= 4) return pick<2, 4>();
+#ifndef MPCQP_ONLY_SMALL
+  if (rn <= 4 && rm <= 8) return pick<4, 8>();
+  if (rn <= 8 && rm <= 16) return pick<8, 16>();
+#endif
+  return nullptr;
+}
+
+template <typename T>
+size_t push_blob(std::vector<char>& blob, const std::vector<T>& v) {
+  size_t off = (blob.size() + 15) & ~size_t(15);
+  blob.resize(off + v.size() * sizeof(T) + 16);
+  if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+  return off;
+}
+
+}  // namespace
+
+struct mpcqp_handle {
+  Plan plan;
+  mpcqp_settings set;
+  int B = 0;
+  hipStream_t stream = nullptr;
+  char* d_blob = nullptr;
+  DevPlan dp{};
+  double *Px = nullptr, *q = nullptr, *Ax = nullptr, *l = nullptr, *u = nullptr;
+  double *xs = nullptr, *zs = nullptr, *ys = nullptr, *rho = nullptr, *Ecls = nullptr;
+  int32_t* has_state = nullptr;
+  double* scratch = nullptr;
+  unsigned int* counter = nullptr;
+  bool has_data = false;
+  int grid = 0, lds_bytes = 0, waves_per_cu = 0, wpg = 1;
+  kernel_fn kern = nullptr;
+};
+
+extern "C" {
+
+int mpcqp_version(void) { return 100; }
+const char* mpcqp_last_error(void) { return g_err.c_str(); }
+
+const char* mpcqp_status_string(int32_t st) {
+  switch (st) {
+    case MPCQP_SOLVED: return "solved";
+    case MPCQP_SOLVED_INACCURATE: return "solved inaccurate";
+    case MPCQP_PRIMAL_INFEASIBLE_INACCURATE: return "primal infeasible inaccurate";
+    case MPCQP_DUAL_INFEASIBLE_INACCURATE: return "dual infeasible inaccurate";
+    case MPCQP_MAX_ITER_REACHED: return "maximum iterations reached";
+    case MPCQP_PRIMAL_INFEASIBLE: return "primal infeasible";
+    case MPCQP_DUAL_INFEASIBLE: return "dual infeasible";
+    case -5: return "interrupted";
+    case -6: return "run time limit reached";
+    case MPCQP_NON_CVX: return "problem non convex";
+    case MPCQP_UNSOLVED: return "unsolved";
+    default: return "unknown";
+  }
+}
+
+int mpcqp_default_settings(mpcqp_settings* s) {
+  if (!s) return fail(MPCQP_E_INVALID, "null settings");
+  s->rho = 0.1;
+  s->sigma = 1e-06;
+  s->alpha = 1.6;
+  s->eps_abs = 1e-3;
+  s->eps_rel = 1e-3;
+  s->eps_prim_inf = 1e-4;
+  s->eps_dual_inf = 1e-4;
+  s->delta = 1e-6;
+  s->adaptive_rho_tolerance = 5;
+  s->max_iter = 4000;
+  s->scaling = 10;
+  s->adaptive_rho = 1;
+  s->adaptive_rho_interval = 0;
+  s->polish = 0;
+  s->polish_refine_iter = 3;
+  s->check_termination = 25;
+  s->warm_start = 1;
+  s->scaled_termination = 0;
+  return 0;
+}
+
+int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t batch, void* stream,
+                 mpcqp_handle** out) {
+  if (!st || !s || !out || batch <= 0) return fail(MPCQP_E_INVALID, "invalid argument");
+  *out = nullptr;
+  if (st->m <= 0) return fail(MPCQP_E_UNSUPPORTED, "problems without constraints (m == 0)");
+  if (s->polish) return fail(MPCQP_E_UNSUPPORTED, "polish is not implemented in this build");
+  if (s->scaled_termination)
+    return fail(MPCQP_E_UNSUPPORTED, "scaled_termination is not implemented in this build");
+  if (s->max_iter <= 0 || s->alpha <= 0 || s->alpha >= 2 || s->sigma <= 0 || s->rho <= 0 ||
+      s->scaling < 0 || s->check_termination < 0 || s->eps_abs < 0 || s->eps_rel < 0)
+    return fail(MPCQP_E_INVALID, "invalid settings");
+  mpcqp_handle* h = new mpcqp_handle();
+  h->set = *s;
+  h->B = batch;
+  h->stream = (hipStream_t)stream;
+  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, MAXC, MAXC3, h->plan)) {
+    std::string e = h->plan.error;
+    delete h;
+    return fail(MPCQP_E_UNSUPPORTED, e);
+  }
+  const Plan& pl = h->plan;
+  h->kern = select_kernel(pl.n, pl.m);
+  if (!h->kern) {
+    delete h;
+    return fail(MPCQP_E_UNSUPPORTED, "problem dimensions exceed the instantiated kernels");
+  }
+  // structure blob
+  std::vector<char> blob;
+  size_t o_fac = push_blob(blob, pl.fac), o_fwd = push_blob(blob, pl.fwd),
+         o_bwd = push_blob(blob, pl.bwd), o_meta = push_blob(blob, pl.meta),
+         o_t2 = push_blob(blob, pl.terms2), o_t3 = push_blob(blob, pl.terms3),
+         o_sP = push_blob(blob, pl.slotP), o_sA = push_blob(blob, pl.slotA),
+         o_sR = push_blob(blob, pl.slotRho), o_sS = push_blob(blob, pl.slotSig),
+         o_wx = push_blob(blob, pl.wsx), o_wz = push_blob(blob, pl.wsz),
+         o_Ap = push_blob(blob, pl.Ap), o_Ai = push_blob(blob, pl.Ai),
+         o_Ac = push_blob(blob, pl.Acol), o_Arp = push_blob(blob, pl.Arp),
+         o_Ark = push_blob(blob, pl.Ark), o_Arj = push_blob(blob, pl.Arj),
+         o_Pi = push_blob(blob, pl.Pi), o_Pc = push_blob(blob, pl.Pcol),
+         o_Psp = push_blob(blob, pl.Psp), o_Psk = push_blob(blob, pl.Psk),
+         o_Pso = push_blob(blob, pl.Pso), o_sm = push_blob(blob, pl.smeta),
+         o_st = push_blob(blob, pl.sterms);
+  auto cleanup_fail = [&](int code, const std::string& msg) {
+    mpcqp_destroy(h);
+    return fail(code, msg);
+  };
+  if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
+    return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
+  if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup_fail(MPCQP_E_HIP, "hipMemcpy(structure)");
+  char* b = h->d_blob;
+  DevPlan& dp = h->dp;
+  dp.fac = (const StepHdr*)(b + o_fac), dp.fwd = (const StepHdr*)(b + o_fwd);
+  dp.bwd = (const StepHdr*)(b + o_bwd);
+  dp.nfac = (int)pl.fac.size(), dp.nfwd = (int)pl.fwd.size(), dp.nbwd = (int)pl.bwd.size();
+  dp.meta = (const uint32_t*)(b + o_meta), dp.terms2 = (const uint32_t*)(b + o_t2);
+  dp.terms3 = (const uint64_t*)(b + o_t3);
+  dp.slotP = (const uint16_t*)(b + o_sP), dp.slotA = (const uint16_t*)(b + o_sA);
+  dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
+  dp.wsx = (const uint16_t*)(b + o_wx), dp.wsz = (const uint16_t*)(b + o_wz);
+  dp.Ap = (const uint16_t*)(b + o_Ap), dp.Ai = (const uint16_t*)(b + o_Ai);
+  dp.Acol = (const uint16_t*)(b + o_Ac), dp.Arp = (const uint16_t*)(b + o_Arp);
+  dp.Ark = (const uint16_t*)(b + o_Ark), dp.Arj = (const uint16_t*)(b + o_Arj);
+  dp.Pi = (const uint16_t*)(b + o_Pi), dp.Pcol = (const uint16_t*)(b + o_Pc);
+  dp.Psp = (const uint16_t*)(b + o_Psp), dp.Psk = (const uint16_t*)(b + o_Psk);
+  dp.Pso = (const uint16_t*)(b + o_Pso);
+  dp.smeta = (const uint32_t*)(b + o_sm), dp.sterms = (const uint32_t*)(b + o_st);
+  dp.nsmeta = (int)pl.smeta.size(), dp.nsterms = (int)pl.sterms.size();
+  dp.hdr_words = 4 * (dp.nfwd + dp.nbwd + dp.nfac);
+  dp.tbl_words = (dp.hdr_words + dp.nsmeta + dp.nsterms + 3) & ~3;
+  dp.inst_doubles = (pl.LDS_N + 1) & ~1;
+  dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
+  dp.nnzL = pl.nnzL;
+  dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.ZERO = pl.ZERO, dp.LDS_N = pl.LDS_N;
+  dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
+
+  // occupancy -> workgroup size (waves sharing one LDS copy of the solve tables) and grid
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return cleanup_fail(MPCQP_E_HIP, "hipGetDevice");
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return cleanup_fail(MPCQP_E_HIP, "hipDeviceGetAttribute");
+  const int tbl_bytes = dp.tbl_words * 4, inst_bytes = dp.inst_doubles * 8;
+  const int lds_cap = 160 * 1024;
+  if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          lds_cap) != hipSuccess)
+    return cleanup_fail(MPCQP_E_HIP, "hipFuncSetAttribute");
+  int best_waves = 0, best_wpg = 0, best_nb = 0;
+  for (int wpg = 1; wpg <= 8; ++wpg) {
+    const int lds = tbl_bytes + wpg * inst_bytes;
+    if (lds > lds_cap) break;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, 64 * wpg, lds) !=
+        hipSuccess)
+      continue;
+    if (nb * wpg > best_waves) best_waves = nb * wpg, best_wpg = wpg, best_nb = nb;
+  }
+  if (best_waves <= 0)
+    return cleanup_fail(MPCQP_E_UNSUPPORTED, "kernel does not fit on a CU (LDS/VGPR)");
+  h->wpg = best_wpg;
+  h->waves_per_cu = best_waves;
+  h->lds_bytes = tbl_bytes + best_wpg * inst_bytes;
+  h->grid = std::min((batch + best_wpg - 1) / best_wpg, best_nb * ncu);
+  const size_t Bz = (size_t)batch;
+  bool ok = hipMalloc(&h->Px, sizeof(double) * std::max(1, pl.nnzP)) == hipSuccess &&
+            hipMalloc(&h->q, sizeof(double) * pl.n) == hipSuccess &&
+            hipMalloc(&h->Ax, sizeof(double) * Bz * std::max(1, pl.nnzA)) == hipSuccess &&
+            hipMalloc(&h->l, sizeof(double) * Bz * pl.m) == hipSuccess &&
+            hipMalloc(&h->u, sizeof(double) * Bz * pl.m) == hipSuccess &&
+            hipMalloc(&h->xs, sizeof(double) * Bz * pl.n) == hipSuccess &&
+            hipMalloc(&h->zs, sizeof(double) * Bz * pl.m) == hipSuccess &&
+            hipMalloc(&h->ys, sizeof(double) * Bz * pl.m) == hipSuccess &&
+            hipMalloc(&h->Ecls, sizeof(double) * Bz * pl.m) == hipSuccess &&
+            hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
+            hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
+            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid * h->wpg *
+                                       (pl.nnzP + pl.nnzA + 2 * pl.n + 2 * pl.m)) ==
+                hipSuccess &&
+            hipMalloc(&h->counter, 64) == hipSuccess;
+  if (!ok) return cleanup_fail(MPCQP_E_HIP, "hipMalloc(batch buffers)");
+  if (hipMemset(h->has_state, 0, sizeof(int32_t) * Bz) != hipSuccess)
+    return cleanup_fail(MPCQP_E_HIP, "hipMemset");
+  *out = h;
+  return 0;
+}
+
+int mpcqp_destroy(mpcqp_handle* h) {
+  if (!h) return 0;
+  void* bufs[] = {h->d_blob, h->Px, h->q,    h->Ax,        h->l,       h->u,      h->xs,
+                  h->zs,     h->ys, h->Ecls, h->rho, h->has_state, h->scratch, h->counter};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  delete h;
+  return 0;
+}
+
+int mpcqp_set_data(mpcqp_handle* h, const double* Px, const double* q, const double* Ax,
+                   const double* l, const double* u) {
+  if (!h || !Px || !q || !Ax || !l || !u) return fail(MPCQP_E_INVALID, "null argument");
+  const Plan& pl = h->plan;
+  const size_t B = (size_t)h->B;
+  HIPCHK(hipMemcpyAsync(h->Px, Px, sizeof(double) * pl.nnzP, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->q, q, sizeof(double) * pl.n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->Ax, Ax, sizeof(double) * B * pl.nnzA, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->l, l, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->u, u, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemsetAsync(h->has_state, 0, sizeof(int32_t) * B, h->stream));
+  h->has_data = true;
+  return 0;
+}
+
+int mpcqp_update_bounds(mpcqp_handle* h, const double* l, const double* u) {
+  if (!h || !l || !u) return fail(MPCQP_E_INVALID, "null argument");
+  if (!h->has_data) return fail(MPCQP_E_NODATA, "update before set_data");
+  const size_t B = (size_t)h->B;
+  HIPCHK(hipMemcpyAsync(h->l, l, sizeof(double) * B * h->plan.m, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->u, u, sizeof(double) * B * h->plan.m, hipMemcpyDeviceToDevice, h->stream));
+  return 0;
+}
+
+int mpcqp_update_A(mpcqp_handle* h, const double* Ax) {
+  if (!h || !Ax) return fail(MPCQP_E_INVALID, "null argument");
+  if (!h->has_data) return fail(MPCQP_E_NODATA, "update before set_data");
+  HIPCHK(hipMemcpyAsync(h->Ax, Ax, sizeof(double) * (size_t)h->B * h->plan.nnzA,
+                        hipMemcpyDeviceToDevice, h->stream));
+  return 0;
+}
+
+int mpcqp_update_lin_cost(mpcqp_handle* h, const double* q) {
+  if (!h || !q) return fail(MPCQP_E_INVALID, "null argument");
+  if (!h->has_data) return fail(MPCQP_E_NODATA, "update before set_data");
+  HIPCHK(hipMemcpyAsync(h->q, q, sizeof(double) * h->plan.n, hipMemcpyDeviceToDevice, h->stream));
+  return 0;
+}
+
+int mpcqp_warm_start(mpcqp_handle* h, const double* x, const double* y) {
+  if (!h || !x || !y) return fail(MPCQP_E_INVALID, "null argument");
+  if (!h->has_data) return fail(MPCQP_E_NODATA, "warm start before set_data");
+  const size_t B = (size_t)h->B;
+  HIPCHK(hipMemcpyAsync(h->xs, x, sizeof(double) * B * h->plan.n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->ys, y, sizeof(double) * B * h->plan.m, hipMemcpyDeviceToDevice, h->stream));
+  // has_state = 2 for every instance, but keep rho: a warm start does not reset rho in OSQP.
+  // (rho_state is only read when has_state != 0; instances never solved start from settings.rho)
+  std::vector<int32_t> two(B, 2);
+  HIPCHK(hipMemcpyAsync(h->has_state, two.data(), sizeof(int32_t) * B, hipMemcpyHostToDevice,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  if (!h->has_data) return fail(MPCQP_E_NODATA, "solve before set_data");
+  KParams p{};
+  p.pl = h->dp;
+  p.s = h->set;
+  p.B = h->B;
+  p.Px = h->Px, p.q = h->q, p.Ax = h->Ax, p.l = h->l, p.u = h->u;
+  p.xs = h->xs, p.zs = h->zs, p.ys = h->ys, p.rho_state = h->rho, p.Ecls = h->Ecls;
+  p.has_state = h->has_state;
+  p.x_out = x, p.y_out = y;
+  if (info) p.info = *info;
+  p.scratch = h->scratch;
+  p.counter = h->counter;
+  HIPCHK(hipMemsetAsync(h->counter, 0, 64, h->stream));
+  hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(64 * h->wpg), h->lds_bytes, h->stream, p);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int mpcqp_dims(const mpcqp_handle* h, int32_t* n, int32_t* m, int32_t* nnzP, int32_t* nnzA,
+               int32_t* nnzL) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  if (n) *n = h->plan.n;
+  if (m) *m = h->plan.m;
+  if (nnzP) *nnzP = h->plan.nnzP;
+  if (nnzA) *nnzA = h->plan.nnzA;
+  if (nnzL) *nnzL = h->plan.nnzL;
+  return 0;
+}
+
+int mpcqp_schedule_info(const mpcqp_handle* h, int32_t* fac, int32_t* fwd, int32_t* bwd,
+                        int32_t* lds, int32_t* wpc) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  if (fac) *fac = (int32_t)h->plan.fac.size();
+  if (fwd) *fwd = (int32_t)h->plan.fwd.size();
+  if (bwd) *bwd = (int32_t)h->plan.bwd.size();
+  if (lds) *lds = h->lds_bytes;
+  if (wpc) *wpc = h->waves_per_cu;
+  return 0;
+}
+
+int mpcqp_export_symbolic(const mpcqp_handle* h, int32_t* perm, int32_t* Lp, int32_t* Li) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  const Plan& pl = h->plan;
+  if (perm) std::copy(pl.perm.begin(), pl.perm.end(), perm);
+  if (Lp) std::copy(pl.Lp.begin(), pl.Lp.end(), Lp);
+  if (Li) std::copy(pl.Li.begin(), pl.Li.end(), Li);
+  return 0;
+}
+
+}  // extern "C"

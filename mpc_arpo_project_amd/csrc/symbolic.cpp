@@ -1,0 +1,419 @@
+// symbolic.cpp -- see symbolic.hpp.
+#include "symbolic.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <numeric>
+#include <unordered_map>
+
+namespace mpcqp {
+namespace {
+
+// Exact minimum-degree ordering, lowest index wins ties.  Identical to the oracle's
+// min_degree_order (oracle/osqp_oracle.c), so the device factor has the oracle's sparsity.
+void min_degree(int nk, std::vector<uint8_t>& adj, std::vector<int32_t>& perm) {
+  std::vector<uint8_t> alive(nk, 1);
+  std::vector<int> deg(nk, 0), nbr(nk);
+  for (int i = 0; i < nk; i++) {
+    int d = 0;
+    for (int j = 0; j < nk; j++) d += adj[(size_t)i * nk + j];
+    deg[i] = d;
+  }
+  perm.assign(nk, 0);
+  for (int k = 0; k < nk; k++) {
+    int best = -1;
+    for (int i = 0; i < nk; i++)
+      if (alive[i] && (best < 0 || deg[i] < deg[best])) best = i;
+    perm[k] = best;
+    alive[best] = 0;
+    int cnt = 0;
+    for (int j = 0; j < nk; j++)
+      if (alive[j] && adj[(size_t)best * nk + j]) nbr[cnt++] = j;
+    for (int a = 0; a < cnt; a++) {
+      int ia = nbr[a];
+      adj[(size_t)ia * nk + best] = 0;
+      for (int b = 0; b < cnt; b++) {
+        int ib = nbr[b];
+        if (ia != ib && !adj[(size_t)ia * nk + ib]) {
+          adj[(size_t)ia * nk + ib] = 1;
+          deg[ia]++;
+        }
+      }
+      deg[ia]--;
+    }
+  }
+}
+
+struct Task {
+  uint32_t target;
+  bool isD;
+  std::vector<uint64_t> terms;  // packed a | b << 16 | c << 32
+};
+
+// Pack one level's tasks into 64-lane steps (see symbolic.hpp).
+void pack_level(std::vector<Task>& tasks, StepKind kind, int max_c, int dummy_slot,
+                std::vector<StepHdr>& steps, std::vector<uint32_t>& meta,
+                std::vector<uint32_t>& terms2, std::vector<uint64_t>& terms3) {
+  struct Placed {
+    const Task* t;
+    int g, glog, c;
+  };
+  std::vector<Placed> pl;
+  for (auto& t : tasks) {
+    int nt = (int)t.terms.size();
+    int g = 1, glog = 0;
+    while (g < 64 && (nt + g - 1) / g > max_c) g *= 2, glog++;
+    int c = (nt + g - 1) / g;
+    pl.push_back({&t, g, glog, c});
+  }
+  // widest groups first keeps groups aligned; then by C so that similar tasks share a step
+  std::stable_sort(pl.begin(), pl.end(), [](const Placed& a, const Placed& b) {
+    if (a.g != b.g) return a.g > b.g;
+    return a.c > b.c;
+  });
+  const uint64_t dummy = (uint64_t)dummy_slot | ((uint64_t)dummy_slot << 16) |
+                         ((uint64_t)dummy_slot << 32);
+  size_t i = 0;
+  while (i < pl.size()) {
+    // gather tasks for one step
+    std::vector<std::pair<int, const Placed*>> in;  // lane offset, task
+    int cur = 0, C = 0, glog = 0;
+    while (i < pl.size()) {
+      int off = (cur + pl[i].g - 1) / pl[i].g * pl[i].g;
+      if (off + pl[i].g > 64) break;
+      in.push_back({off, &pl[i]});
+      cur = off + pl[i].g;
+      C = std::max(C, pl[i].c);
+      glog = std::max(glog, pl[i].glog);
+      i++;
+    }
+    int cnt = cur;
+    StepHdr h;
+    h.off_meta = (uint32_t)meta.size();
+    h.off_terms = kind == KIND_DOT3 ? (uint32_t)terms3.size() : (uint32_t)terms2.size();
+    h.cnt = (uint32_t)cnt;
+    h.cfg = (uint32_t)C | ((uint32_t)glog << 8) | ((uint32_t)kind << 16);
+    std::vector<uint32_t> mrow(cnt, 0);
+    std::vector<uint64_t> trow((size_t)C * cnt, dummy);
+    for (auto& pr : in) {
+      int off = pr.first;
+      const Placed* p = pr.second;
+      for (int r = 0; r < p->g; r++) {
+        uint32_t mt = META_ACTIVE | ((uint32_t)p->glog << META_GLOG_SHIFT);
+        mt |= p->t->target & META_TGT_MASK;
+        if (r == 0) mt |= META_HEAD;
+        if (p->t->isD) mt |= META_ISD;
+        mrow[off + r] = mt;
+      }
+      const auto& tv = p->t->terms;
+      for (size_t q = 0; q < tv.size(); q++) {
+        int lane = off + (int)(q % p->g);
+        int c = (int)(q / p->g);
+        trow[(size_t)c * cnt + lane] = tv[q];
+      }
+    }
+    meta.insert(meta.end(), mrow.begin(), mrow.end());
+    if (kind == KIND_DOT3) {
+      terms3.insert(terms3.end(), trow.begin(), trow.end());
+    } else {
+      for (auto t : trow) terms2.push_back((uint32_t)(t & 0xffffffffu));
+    }
+    steps.push_back(h);
+  }
+}
+
+void pack_scale(const std::vector<uint32_t>& entries, std::vector<StepHdr>& steps,
+                std::vector<uint32_t>& terms2) {
+  for (size_t s = 0; s < entries.size(); s += 64) {
+    size_t cnt = std::min<size_t>(64, entries.size() - s);
+    StepHdr h;
+    h.off_meta = 0;
+    h.off_terms = (uint32_t)terms2.size();
+    h.cnt = (uint32_t)cnt;
+    h.cfg = 1u | ((uint32_t)KIND_SCALE << 16);
+    terms2.insert(terms2.end(), entries.begin() + s, entries.begin() + s + cnt);
+    steps.push_back(h);
+  }
+}
+
+}  // namespace
+
+bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                const int32_t* Ai, int max_c, int max_c3, Plan& pl) {
+  pl = Plan();
+  pl.n = n, pl.m = m, pl.nk = n + m;
+  const int nk = n + m;
+  pl.nnzP = Pp[n];
+  pl.nnzA = Ap[n];
+  if (n <= 0 || m < 0) {
+    pl.error = "empty problem";
+    return false;
+  }
+  for (int j = 0; j < n; j++) {
+    for (int p = Pp[j]; p < Pp[j + 1]; p++) {
+      if (Pi[p] < 0 || Pi[p] > j) {
+        pl.error = "P must be upper triangular CSC";
+        return false;
+      }
+      if (p > Pp[j] && Pi[p] <= Pi[p - 1]) {
+        pl.error = "P row indices must be sorted and unique";
+        return false;
+      }
+    }
+    for (int p = Ap[j]; p < Ap[j + 1]; p++) {
+      if (Ai[p] < 0 || Ai[p] >= m) {
+        pl.error = "A row index out of range";
+        return false;
+      }
+      if (p > Ap[j] && Ai[p] <= Ai[p - 1]) {
+        pl.error = "A row indices must be sorted and unique";
+        return false;
+      }
+    }
+  }
+  if (pl.nnzA >= 65535 || pl.nnzP >= 65535 || nk >= 65535) {
+    pl.error = "problem too large for 16-bit schedule indices";
+    return false;
+  }
+
+  // ---- ordering on the symmetric KKT pattern
+  std::vector<uint8_t> adj((size_t)nk * nk, 0);
+  for (int j = 0; j < n; j++)
+    for (int p = Pp[j]; p < Pp[j + 1]; p++)
+      if (Pi[p] != j) adj[(size_t)Pi[p] * nk + j] = adj[(size_t)j * nk + Pi[p]] = 1;
+  for (int j = 0; j < n; j++)
+    for (int p = Ap[j]; p < Ap[j + 1]; p++) {
+      int r = n + Ai[p];
+      adj[(size_t)r * nk + j] = adj[(size_t)j * nk + r] = 1;
+    }
+  min_degree(nk, adj, pl.perm);
+  adj.clear();
+  adj.shrink_to_fit();
+  pl.pinv.assign(nk, 0);
+  for (int k = 0; k < nk; k++) pl.pinv[pl.perm[k]] = k;
+
+  // ---- permuted KKT pattern (lower triangle as rows of K, i > j) in permuted coordinates
+  std::vector<std::vector<int>> krow(nk);  // krow[i] = {j < i : K_ij != 0}
+  auto add_edge = [&](int a, int b) {
+    int pa = pl.pinv[a], pb = pl.pinv[b];
+    if (pa == pb) return;
+    int i = std::max(pa, pb), j = std::min(pa, pb);
+    krow[i].push_back(j);
+  };
+  for (int j = 0; j < n; j++)
+    for (int p = Pp[j]; p < Pp[j + 1]; p++)
+      if (Pi[p] != j) add_edge(Pi[p], j);
+  for (int j = 0; j < n; j++)
+    for (int p = Ap[j]; p < Ap[j + 1]; p++) add_edge(n + Ai[p], j);
+
+  // ---- elimination tree + row patterns of L (row subtree traversal)
+  pl.etree.assign(nk, -1);
+  std::vector<int> flag(nk, -1), anc(nk, -1);
+  std::vector<std::vector<int>> lrow(nk);  // lrow[i] = {k < i : L_ik != 0}, sorted
+  for (int i = 0; i < nk; i++) {
+    flag[i] = i;
+    for (int j0 : krow[i]) {
+      for (int j = j0; flag[j] != i; j = pl.etree[j]) {
+        if (pl.etree[j] == -1) pl.etree[j] = i;
+        lrow[i].push_back(j);
+        flag[j] = i;
+      }
+    }
+    std::sort(lrow[i].begin(), lrow[i].end());
+  }
+  (void)anc;
+  // column patterns
+  std::vector<std::vector<int>> lcol(nk);
+  for (int i = 0; i < nk; i++)
+    for (int k : lrow[i]) lcol[k].push_back(i);  // ascending i
+  pl.Lp.assign(nk + 1, 0);
+  for (int j = 0; j < nk; j++) pl.Lp[j + 1] = pl.Lp[j] + (int)lcol[j].size();
+  pl.nnzL = pl.Lp[nk];
+  pl.Li.resize(pl.nnzL);
+  for (int j = 0; j < nk; j++)
+    std::copy(lcol[j].begin(), lcol[j].end(), pl.Li.begin() + pl.Lp[j]);
+  auto lpos = [&](int i, int j) -> int {  // position of L_ij (i > j) in Li/Lx
+    auto b = pl.Li.begin() + pl.Lp[j], e = pl.Li.begin() + pl.Lp[j + 1];
+    auto it = std::lower_bound(b, e, i);
+    return (it != e && *it == i) ? (int)(it - pl.Li.begin()) : -1;
+  };
+
+  // ---- LDS layout (doubles)
+  pl.LX = 0;
+  pl.DINV = pl.nnzL;
+  pl.W = pl.DINV + nk;
+  pl.ZERO = pl.W + nk;
+  pl.LDS_N = pl.ZERO + 2;  // +1 pad keeps the total even
+  // scaling overlay
+  pl.S_P = 0;
+  pl.S_A = pl.S_P + pl.nnzP;
+  pl.S_DT = pl.S_A + pl.nnzA;
+  pl.S_ET = pl.S_DT + n;
+  if (pl.S_ET + m > pl.LDS_N) pl.LDS_N = pl.S_ET + m;
+  // the residual SpMVs stage x (n) and y (m) as plain arrays in the W region: W + [0, n + m)
+  if (pl.LDS_N >= 65535) {
+    pl.error = "LDS image too large for 16-bit slots";
+    return false;
+  }
+
+  // ---- KKT assembly maps
+  pl.slotP.resize(pl.nnzP);
+  pl.slotSig.resize(n);
+  for (int j = 0; j < n; j++) pl.slotSig[j] = (uint16_t)(pl.W + pl.pinv[j]);
+  for (int j = 0; j < n; j++)
+    for (int p = Pp[j]; p < Pp[j + 1]; p++) {
+      int i = Pi[p];
+      if (i == j) {
+        pl.slotP[p] = (uint16_t)(pl.W + pl.pinv[j]);
+      } else {
+        int a = pl.pinv[i], b = pl.pinv[j];
+        int pos = lpos(std::max(a, b), std::min(a, b));
+        if (pos < 0) {
+          pl.error = "internal: P entry missing from L pattern";
+          return false;
+        }
+        pl.slotP[p] = (uint16_t)(pl.LX + pos);
+      }
+    }
+  pl.slotA.resize(pl.nnzA);
+  for (int j = 0; j < n; j++)
+    for (int p = Ap[j]; p < Ap[j + 1]; p++) {
+      int a = pl.pinv[n + Ai[p]], b = pl.pinv[j];
+      int pos = lpos(std::max(a, b), std::min(a, b));
+      if (pos < 0) {
+        pl.error = "internal: A entry missing from L pattern";
+        return false;
+      }
+      pl.slotA[p] = (uint16_t)(pl.LX + pos);
+    }
+  pl.slotRho.resize(m);
+  for (int i = 0; i < m; i++) pl.slotRho[i] = (uint16_t)(pl.W + pl.pinv[n + i]);
+  pl.wsx.resize(n);
+  pl.wsz.resize(m);
+  for (int i = 0; i < n; i++) pl.wsx[i] = (uint16_t)(pl.W + pl.pinv[i]);
+  for (int i = 0; i < m; i++) pl.wsz[i] = (uint16_t)(pl.W + pl.pinv[n + i]);
+
+  // ---- levels
+  std::vector<int> lev(nk, 0), blev(nk, 0);
+  for (int i = 0; i < nk; i++)
+    for (int k : lrow[i]) lev[i] = std::max(lev[i], lev[k] + 1);
+  for (int j = nk - 1; j >= 0; j--)
+    for (int i : lcol[j]) blev[j] = std::max(blev[j], blev[i] + 1);
+  int maxlev = *std::max_element(lev.begin(), lev.end());
+  int maxblev = *std::max_element(blev.begin(), blev.end());
+  pl.levels_fwd = maxlev + 1;
+  pl.levels_bwd = maxblev + 1;
+  std::vector<std::vector<int>> bylev(maxlev + 1), byblev(maxblev + 1);
+  for (int i = 0; i < nk; i++) bylev[lev[i]].push_back(i), byblev[blev[i]].push_back(i);
+
+  const int Z = pl.ZERO;
+  auto T2 = [](int a, int b) { return (uint64_t)a | ((uint64_t)b << 16); };
+  auto T3 = [](int a, int b, int c) {
+    return (uint64_t)a | ((uint64_t)b << 16) | ((uint64_t)c << 32);
+  };
+
+  // ---- factorization schedule: per level, dot tasks (D_j and numerators of L_ij) then scaling
+  for (int L = 0; L <= maxlev; L++) {
+    std::vector<Task> tasks;
+    std::vector<uint32_t> scal;
+    for (int j : bylev[L]) {
+      Task d;
+      d.target = (uint32_t)(pl.W + j);
+      d.isD = true;
+      for (int k : lrow[j]) {
+        int pjk = lpos(j, k);
+        d.terms.push_back(T3(pl.LX + pjk, pl.LX + pjk, pl.W + k));
+      }
+      tasks.push_back(std::move(d));
+      for (int i : lcol[j]) {
+        Task t;
+        t.target = (uint32_t)(pl.LX + lpos(i, j));
+        t.isD = false;
+        // k in lrow[j] ∩ lrow[i]
+        const auto& a = lrow[j];
+        const auto& b = lrow[i];
+        size_t x = 0, y = 0;
+        while (x < a.size() && y < b.size()) {
+          if (a[x] < b[y])
+            x++;
+          else if (a[x] > b[y])
+            y++;
+          else {
+            int k = a[x];
+            t.terms.push_back(T3(pl.LX + lpos(i, k), pl.LX + lpos(j, k), pl.W + k));
+            x++, y++;
+          }
+        }
+        if (!t.terms.empty()) tasks.push_back(std::move(t));
+        scal.push_back((uint32_t)(pl.LX + lpos(i, j)) | ((uint32_t)(pl.DINV + j) << 16));
+      }
+    }
+    pack_level(tasks, KIND_DOT3, max_c3, Z, pl.fac, pl.meta, pl.terms2, pl.terms3);
+    pack_scale(scal, pl.fac, pl.terms2);
+  }
+  // ---- forward solve L w = b
+  for (int L = 1; L <= maxlev; L++) {
+    std::vector<Task> tasks;
+    for (int i : bylev[L]) {
+      Task t;
+      t.target = (uint32_t)(pl.W + i);
+      t.isD = false;
+      for (int k : lrow[i]) t.terms.push_back(T2(pl.LX + lpos(i, k), pl.W + k));
+      tasks.push_back(std::move(t));
+    }
+    pack_level(tasks, KIND_DOT2, max_c, Z, pl.fwd, pl.smeta, pl.sterms, pl.terms3);
+  }
+  // ---- backward solve L' x = w
+  for (int L = 1; L <= maxblev; L++) {
+    std::vector<Task> tasks;
+    for (int j : byblev[L]) {
+      Task t;
+      t.target = (uint32_t)(pl.W + j);
+      t.isD = false;
+      for (int i : lcol[j]) t.terms.push_back(T2(pl.LX + lpos(i, j), pl.W + i));
+      tasks.push_back(std::move(t));
+    }
+    pack_level(tasks, KIND_DOT2, max_c, Z, pl.bwd, pl.smeta, pl.sterms, pl.terms3);
+  }
+
+  // ---- matrix structure for scaling / residuals
+  pl.Ap.resize(n + 1);
+  pl.Ai.resize(pl.nnzA);
+  pl.Acol.resize(pl.nnzA);
+  for (int j = 0; j <= n; j++) pl.Ap[j] = (uint16_t)Ap[j];
+  for (int j = 0; j < n; j++)
+    for (int p = Ap[j]; p < Ap[j + 1]; p++) pl.Ai[p] = (uint16_t)Ai[p], pl.Acol[p] = (uint16_t)j;
+  std::vector<int> rc(m + 1, 0);
+  for (int p = 0; p < pl.nnzA; p++) rc[Ai[p] + 1]++;
+  for (int i = 0; i < m; i++) rc[i + 1] += rc[i];
+  pl.Arp.resize(m + 1);
+  for (int i = 0; i <= m; i++) pl.Arp[i] = (uint16_t)rc[i];
+  pl.Ark.resize(pl.nnzA);
+  pl.Arj.resize(pl.nnzA);
+  std::vector<int> nx(rc.begin(), rc.end() - 1);
+  for (int j = 0; j < n; j++)
+    for (int p = Ap[j]; p < Ap[j + 1]; p++) {
+      int q = nx[Ai[p]]++;
+      pl.Ark[q] = (uint16_t)p;
+      pl.Arj[q] = (uint16_t)j;
+    }
+  pl.Pi.resize(pl.nnzP);
+  pl.Pcol.resize(pl.nnzP);
+  std::vector<std::vector<std::pair<int, int>>> sym(n);  // per column: (position, other index)
+  for (int j = 0; j < n; j++)
+    for (int p = Pp[j]; p < Pp[j + 1]; p++) {
+      int i = Pi[p];
+      pl.Pi[p] = (uint16_t)i;
+      pl.Pcol[p] = (uint16_t)j;
+      sym[j].push_back({p, i});
+      if (i != j) sym[i].push_back({p, j});
+    }
+  pl.Psp.assign(n + 1, 0);
+  for (int j = 0; j < n; j++) {
+    pl.Psp[j + 1] = (uint16_t)(pl.Psp[j] + sym[j].size());
+    for (auto& e : sym[j]) pl.Psk.push_back((uint16_t)e.first), pl.Pso.push_back((uint16_t)e.second);
+  }
+  return true;
+}
+
+}  // namespace mpcqp
