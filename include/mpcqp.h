@@ -119,6 +119,16 @@ int mpcqp_warm_start(mpcqp_handle *h, const double *x, const double *y);
  * x [B*n], y [B*m] device outputs (unscaled, NaN when no solution exists, as OSQP). */
 int mpcqp_solve(mpcqp_handle *h, double *x, double *y, const mpcqp_info *info);
 
+/* Zero-copy access to the handle's own problem-data buffers (device): Ax [B*nnzA], l, u [B*m].
+ * A producer kernel (e.g. mpcqp_cl_configure) may rewrite them in place between solves, on the
+ * handle's stream; the next mpcqp_solve re-scales and re-factors from them (osqp_update_A +
+ * osqp_update_bounds semantics). */
+int mpcqp_data_buffers(mpcqp_handle *h, double **Ax, double **l, double **u);
+
+/* Copy the current problem data of every instance into caller device buffers (any may be NULL):
+ * Ax [B*nnzA], l, u [B*m]. */
+int mpcqp_copy_data(mpcqp_handle *h, double *Ax, double *l, double *u);
+
 /* Introspection. */
 int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA,
                int32_t *nnzL);
@@ -126,6 +136,12 @@ int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int
  * triangular solves, LDS bytes per instance and resident waves (instances in flight) per CU. */
 int mpcqp_schedule_info(const mpcqp_handle *h, int32_t *fac_steps, int32_t *fwd_steps,
                         int32_t *bwd_steps, int32_t *lds_bytes, int32_t *waves_per_cu);
+/* Host-only symbolic analysis (no HIP call; usable without a GPU): KKT ordering, L pattern and
+ * schedule statistics for a structure.  perm [n+m], Lp [n+m+1] may be NULL; Li is written only
+ * when non-NULL and *nnzL (in) >= the true count.  stats (may be NULL) receives
+ * {fac_steps, fwd_steps, bwd_steps, fwd_levels, bwd_levels, lds_image_bytes}. */
+int mpcqp_analyze(const mpcqp_structure *st, int32_t *perm, int32_t *Lp, int32_t *Li,
+                  int32_t *nnzL, int32_t *stats);
 /* Host-side export of the symbolic analysis for white-box tests (no device work):
  * perm [n+m] (KKT position -> original KKT index), Lp [n+m+1], Li [nnzL]. */
 int mpcqp_export_symbolic(const mpcqp_handle *h, int32_t *perm, int32_t *Lp, int32_t *Li);

@@ -1,0 +1,61 @@
+/*
+ * mpcqp_closed_loop.h -- C ABI of the device-side closed-loop step that surrounds the QP solve
+ * (part of libmpcqp.so).  These kernels replace, for a batch of independent chasers:
+ *
+ *   mpcqp_cl_configure  <- configureDynamicConstraints(...) + the l/u splice
+ *                          reference src/simhelpers.py:11-140, src/trajectorySimulate.py:339-347
+ *   mpcqp_cl_step       <- controller select (MPC / LQR failsafe / deadbeat), input-norm clip,
+ *                          discrete linear CW plant, perfect-state estimate, termination test
+ *                          reference src/trajectorySimulate.py:285-337 (noise=None path)
+ *
+ * Per-instance arrays are device pointers, row-major [instance][k].  Scenario constants are
+ * host values copied into the handle at creation.  Planar model only: nx = 4, nu = 2, ny = 5,
+ * ndi = 2 (the reference's model, src/trajectorySimulate.py:73-97).
+ */
+#ifndef MPCQP_CLOSED_LOOP_H
+#define MPCQP_CLOSED_LOOP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  int32_t Nx, Nc, Nb, m, nnzA;
+  double Ad[16], Bd[8];          /* row-major 4x4, 4x2 */
+  double rp, rtol, xr[4];        /* platform radius, tolerance radius, reference state */
+  int32_t inTrack, isReject, has_debris;
+  double center[2], side, detect; /* debris box as given (un-swapped) */
+  double verts[8];                /* debris vertices in configureDynamicConstraints' order
+                                     (already turned on its side for in-track runs) */
+  double umin[7], umax[7];        /* bounds of one (u, s) block */
+  double Kpf[8], Kif[2];          /* failsafe LQR with integral action, 2x4 and 2x1 */
+  double Ktot[8], Ki[2];          /* deadbeat debris avoidance, 2x4 and 2x1 */
+  double Crefx[4], Crefy[4];
+  const int32_t *pos_c1, *pos_c2, *pos_slope; /* host, Nx+1 each: CSC positions of the varying
+                                                 A values (pos_slope NULL when no debris) */
+} mpcqp_cl_scenario;
+
+typedef struct mpcqp_cl mpcqp_cl;
+
+int mpcqp_cl_create(const mpcqp_cl_scenario *sc, int32_t batch, void *stream, mpcqp_cl **out);
+int mpcqp_cl_destroy(mpcqp_cl *cl);
+
+/* From estimates xest [B*6] = [x, y, vx, vy, dx, dy] write the varying A values into Ax [B*nnzA]
+ * (the constant values must already be there) and the varying bounds into l, u [B*m] (the
+ * constant rows must already be there).  In-track runs swap xest[0] and xest[1] in place afterwards
+ * (reference quirk, src/simhelpers.py:72). */
+int mpcqp_cl_configure(mpcqp_cl *cl, double *xest, double *Ax, double *l, double *u);
+
+/* One control step after a solve.  Inputs: status [B], x_sol [B*n] (u0 read at u0_offset).
+ * State in/out: x_true [B*4], ctrl_prev [B*2] (the control applied this step: one-sample delay,
+ * src/trajectorySimulate.py:323-324), xintf [B], xest [B*6], done [B] (1 once the termination
+ * test fired; such instances are frozen), ctrl_seq [B] (1 MPC, 2 failsafe, 3 deadbeat; output),
+ * ctrl_out [B*2] (the control chosen this step). */
+int mpcqp_cl_step(mpcqp_cl *cl, const int32_t *status, const double *x_sol, int32_t n,
+                  int32_t u0_offset, double *x_true, double *ctrl_prev, double *xintf,
+                  double *xest, int32_t *done, int32_t *ctrl_seq, double *ctrl_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -16,8 +16,9 @@ LIB_PATH = os.path.join(_HERE, "libmpcqp.so")
 EXPORTED = (
     "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",
     "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
-    "mpcqp_solve", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_export_symbolic",
+    "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
     "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version",
+    "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
 )
 
 STATUS = {
@@ -57,6 +58,22 @@ class Info(C.Structure):
                 ("rho", C.c_void_p)]
 
 
+class ClScenario(C.Structure):
+    _fields_ = [
+        ("Nx", C.c_int32), ("Nc", C.c_int32), ("Nb", C.c_int32), ("m", C.c_int32),
+        ("nnzA", C.c_int32),
+        ("Ad", C.c_double * 16), ("Bd", C.c_double * 8),
+        ("rp", C.c_double), ("rtol", C.c_double), ("xr", C.c_double * 4),
+        ("inTrack", C.c_int32), ("isReject", C.c_int32), ("has_debris", C.c_int32),
+        ("center", C.c_double * 2), ("side", C.c_double), ("detect", C.c_double),
+        ("verts", C.c_double * 8), ("umin", C.c_double * 7), ("umax", C.c_double * 7),
+        ("Kpf", C.c_double * 8), ("Kif", C.c_double * 2), ("Ktot", C.c_double * 8),
+        ("Ki", C.c_double * 2), ("Crefx", C.c_double * 4), ("Crefy", C.c_double * 4),
+        ("pos_c1", C.POINTER(C.c_int32)), ("pos_c2", C.POINTER(C.c_int32)),
+        ("pos_slope", C.POINTER(C.c_int32)),
+    ]
+
+
 _lib = None
 
 
@@ -80,8 +97,15 @@ def lib():
     L.mpcqp_warm_start.argtypes = [vp, dp, dp]
     L.mpcqp_solve.argtypes = [vp, dp, dp, C.POINTER(Info)]
     L.mpcqp_dims.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
+    L.mpcqp_copy_data.argtypes = [vp, dp, dp, dp]
+    L.mpcqp_data_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
     L.mpcqp_schedule_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
     L.mpcqp_export_symbolic.argtypes = [vp, i32p, i32p, i32p]
+    L.mpcqp_analyze.argtypes = [C.POINTER(Structure), i32p, i32p, i32p, i32p, i32p]
+    L.mpcqp_cl_create.argtypes = [C.POINTER(ClScenario), i32, vp, C.POINTER(vp)]
+    L.mpcqp_cl_destroy.argtypes = [vp]
+    L.mpcqp_cl_configure.argtypes = [vp, dp, dp, dp, dp]
+    L.mpcqp_cl_step.argtypes = [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp]
     L.mpcqp_status_string.argtypes = [i32]
     L.mpcqp_status_string.restype = C.c_char_p
     L.mpcqp_last_error.restype = C.c_char_p
@@ -111,3 +135,28 @@ def default_settings(**overrides) -> Settings:
             raise ValueError(f"unknown setting '{k}'")
         setattr(s, k, type(getattr(s, k))(v))
     return s
+
+
+def analyze(P_triu_csc, A_csc):
+    """Host-only symbolic analysis (no GPU): perm, Lp, Li and schedule statistics."""
+    import numpy as np
+
+    n, m = P_triu_csc.shape[0], A_csc.shape[0]
+    Pp = np.ascontiguousarray(P_triu_csc.indptr, dtype=np.int32)
+    Pi = np.ascontiguousarray(P_triu_csc.indices, dtype=np.int32)
+    Ap = np.ascontiguousarray(A_csc.indptr, dtype=np.int32)
+    Ai = np.ascontiguousarray(A_csc.indices, dtype=np.int32)
+    i32 = C.POINTER(C.c_int32)
+    st = Structure(n, m, Pp.ctypes.data_as(i32), Pi.ctypes.data_as(i32), Ap.ctypes.data_as(i32),
+                   Ai.ctypes.data_as(i32))
+    perm = np.empty(n + m, dtype=np.int32)
+    Lp = np.empty(n + m + 1, dtype=np.int32)
+    nnz = C.c_int32(0)
+    stats = np.empty(6, dtype=np.int32)
+    check(lib().mpcqp_analyze(C.byref(st), perm.ctypes.data_as(i32), Lp.ctypes.data_as(i32), None,
+                              C.byref(nnz), stats.ctypes.data_as(i32)), "mpcqp_analyze")
+    Li = np.empty(max(nnz.value, 1), dtype=np.int32)
+    check(lib().mpcqp_analyze(C.byref(st), None, None, Li.ctypes.data_as(i32), C.byref(nnz), None),
+          "mpcqp_analyze")
+    keys = ("fac_steps", "fwd_steps", "bwd_steps", "fwd_levels", "bwd_levels", "lds_image_bytes")
+    return perm, Lp, Li[:nnz.value], dict(zip(keys, stats.tolist()))

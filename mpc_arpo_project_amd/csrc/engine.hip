@@ -1345,6 +1345,29 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   return 0;
 }
 
+int mpcqp_data_buffers(mpcqp_handle* h, double** Ax, double** l, double** u) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  if (Ax) *Ax = h->Ax;
+  if (l) *l = h->l;
+  if (u) *u = h->u;
+  return 0;
+}
+
+int mpcqp_copy_data(mpcqp_handle* h, double* Ax, double* l, double* u) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  const size_t B = (size_t)h->B;
+  if (Ax)
+    HIPCHK(hipMemcpyAsync(Ax, h->Ax, sizeof(double) * B * h->plan.nnzA, hipMemcpyDeviceToDevice,
+                          h->stream));
+  if (l)
+    HIPCHK(hipMemcpyAsync(l, h->l, sizeof(double) * B * h->plan.m, hipMemcpyDeviceToDevice,
+                          h->stream));
+  if (u)
+    HIPCHK(hipMemcpyAsync(u, h->u, sizeof(double) * B * h->plan.m, hipMemcpyDeviceToDevice,
+                          h->stream));
+  return 0;
+}
+
 int mpcqp_dims(const mpcqp_handle* h, int32_t* n, int32_t* m, int32_t* nnzP, int32_t* nnzA,
                int32_t* nnzL) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");
@@ -1364,6 +1387,28 @@ int mpcqp_schedule_info(const mpcqp_handle* h, int32_t* fac, int32_t* fwd, int32
   if (bwd) *bwd = (int32_t)h->plan.bwd.size();
   if (lds) *lds = h->lds_bytes;
   if (wpc) *wpc = h->waves_per_cu;
+  return 0;
+}
+
+int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t* Li,
+                  int32_t* nnzL, int32_t* stats) {
+  if (!st || !nnzL) return fail(MPCQP_E_INVALID, "null argument");
+  Plan pl;
+  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, MAXC, MAXC3, pl))
+    return fail(MPCQP_E_UNSUPPORTED, pl.error);
+  const int cap = *nnzL;
+  *nnzL = pl.nnzL;
+  if (perm) std::copy(pl.perm.begin(), pl.perm.end(), perm);
+  if (Lp) std::copy(pl.Lp.begin(), pl.Lp.end(), Lp);
+  if (Li && cap >= pl.nnzL) std::copy(pl.Li.begin(), pl.Li.end(), Li);
+  if (stats) {
+    stats[0] = (int32_t)pl.fac.size();
+    stats[1] = (int32_t)pl.fwd.size();
+    stats[2] = (int32_t)pl.bwd.size();
+    stats[3] = pl.levels_fwd;
+    stats[4] = pl.levels_bwd;
+    stats[5] = pl.LDS_N * (int)sizeof(double);
+  }
   return 0;
 }
 

@@ -150,6 +150,16 @@ class BatchQP:
             keep["Ax"] = Ax
         self._keep(**keep)
 
+    def copy_data(self):
+        """(Ax, l, u) currently held by the handle, as new device tensors."""
+        f = dict(dtype=torch.float64, device=self.device)
+        Ax = torch.empty(self.B, self.nnzA, **f)
+        l = torch.empty(self.B, self.m, **f)
+        u = torch.empty(self.B, self.m, **f)
+        check(_lib.lib().mpcqp_copy_data(self._h, Ax.data_ptr(), l.data_ptr(), u.data_ptr()),
+              "mpcqp_copy_data")
+        return Ax, l, u
+
     def warm_start(self, x, y):
         x = self._batch_vec(x, self.n, "x")
         y = self._batch_vec(y, self.m, "y")
@@ -210,3 +220,11 @@ class BatchQP:
             self.close()
         except Exception:
             pass
+
+
+def data_buffers(qp: BatchQP):
+    """Raw device pointers (ints) of the handle's own Ax / l / u buffers (zero-copy updates)."""
+    a, l, u = C.c_void_p(), C.c_void_p(), C.c_void_p()
+    check(_lib.lib().mpcqp_data_buffers(qp._h, C.byref(a), C.byref(l), C.byref(u)),
+          "mpcqp_data_buffers")
+    return a.value, l.value, u.value

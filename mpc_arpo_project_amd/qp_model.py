@@ -135,6 +135,8 @@ class MPCProblem:
     pos_slope: np.ndarray = field(default=None)
     # scenario constants used by configureDynamicConstraints
     rp: float = 0.0
+    rtol: float = 0.0
+    xr: np.ndarray = None
     rx: float = 0.0
     ry: float = 0.0
     isReject: bool = True
@@ -287,7 +289,8 @@ def build_problem(sim_conditions: SimConditions, mpc_params: MPCParams,
     hd, ctr, sd, det, verts = _debris_geometry(sim_conditions, debris)
     prob = MPCProblem(nx=nx, nu=nu, ny=ny, ndi=ndi, Nx=Nx, Nc=Nc, Nb=Nb, T=T,
                       Ad=Ad_s.toarray(), Bd=Bd_s.toarray(), K=K, S=S, C=C, umin=umin, umax=umax,
-                      P=P, q=q, A=None, l=None, u=None, rp=rp, rx=float(xr[0]), ry=float(xr[1]),
+                      P=P, q=q, A=None, l=None, u=None, rp=rp, rtol=rtot, xr=xr.copy(),
+                      rx=float(xr[0]), ry=float(xr[1]),
                       isReject=bool(sim_conditions.isReject), inTrack=bool(sim_conditions.inTrack),
                       has_debris=hd, center=ctr, side=sd, detect=det, verts=verts)
 

@@ -88,6 +88,9 @@ def lib():
         L.oqp_batch_solve.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip, dp, dp, ip, ip, dp,
                                       dp, dp, C.POINTER(Settings), C.c_int, dp, dp, ip, ip]
         L.oqp_batch_solve.restype = C.c_int
+        L.oqp_batch_update_solve.argtypes = [C.c_int, C.POINTER(C.c_void_p), dp, dp, dp, C.c_int,
+                                             dp, ip, ip]
+        L.oqp_batch_update_solve.restype = C.c_int
         _lib = L
     return _lib
 
@@ -248,3 +251,19 @@ def batch_solve(P, q, A_pattern, Ax_batch, l_batch, u_batch, nthreads=1, **setti
     if rc:
         raise RuntimeError(f"oracle batch solve failed ({rc})")
     return x, y, st, it
+
+
+def batch_update_solve(solvers, Ax_batch, l_batch, u_batch, nthreads=1):
+    """Warm per-step update + solve of a list of OracleOSQP objects in C threads."""
+    B = len(solvers)
+    n = solvers[0].n
+    arr = (C.c_void_p * B)(*[s._w for s in solvers])
+    Ax_batch = np.ascontiguousarray(Ax_batch, dtype=np.float64)
+    l_batch = np.ascontiguousarray(np.maximum(l_batch, -OSQP_INFTY), dtype=np.float64)
+    u_batch = np.ascontiguousarray(np.minimum(u_batch, OSQP_INFTY), dtype=np.float64)
+    x = np.empty((B, n))
+    st = np.empty(B, dtype=np.int32)
+    it = np.empty(B, dtype=np.int32)
+    lib().oqp_batch_update_solve(B, arr, _dp(Ax_batch), _dp(l_batch), _dp(u_batch), nthreads,
+                                 _dp(x), _ip(st), _ip(it))
+    return x, st, it

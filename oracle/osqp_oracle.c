@@ -1273,3 +1273,48 @@ int oqp_batch_solve(int B, int n, int m, const int *Pp, const int *Pi, const dou
   free(jobs);
   return rc;
 }
+
+/* ---------------------------------------------------------------- warm batch driver */
+typedef struct {
+  int b0, b1;
+  oqp_work **works;
+  const double *Ax, *l, *u;
+  double *x;
+  int *status, *iter;
+} warm_job;
+
+static void *warm_worker(void *arg) {
+  warm_job *j = (warm_job *)arg;
+  for (int b = j->b0; b < j->b1; b++) {
+    oqp_work *w = j->works[b];
+    int nnzA = csc_nnz(w->A);
+    oqp_update_bounds(w, j->l + (size_t)b * w->m, j->u + (size_t)b * w->m);
+    oqp_update_A(w, j->Ax + (size_t)b * nnzA);
+    oqp_solve(w);
+    if (j->x) oqp_get_x(w, j->x + (size_t)b * w->n);
+    if (j->status) j->status[b] = w->status;
+    if (j->iter) j->iter[b] = w->iter;
+  }
+  return NULL;
+}
+
+int oqp_batch_update_solve(int B, oqp_work **works, const double *Ax_batch, const double *l_batch,
+                           const double *u_batch, int nthreads, double *x_out, int *status_out,
+                           int *iter_out) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > B) nthreads = B > 0 ? B : 1;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  warm_job *jobs = (warm_job *)calloc((size_t)nthreads, sizeof(warm_job));
+  for (int t = 0; t < nthreads; t++) {
+    warm_job *j = &jobs[t];
+    j->b0 = (int)((long long)B * t / nthreads);
+    j->b1 = (int)((long long)B * (t + 1) / nthreads);
+    j->works = works, j->Ax = Ax_batch, j->l = l_batch, j->u = u_batch;
+    j->x = x_out, j->status = status_out, j->iter = iter_out;
+    pthread_create(&th[t], NULL, warm_worker, j);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+  return 0;
+}

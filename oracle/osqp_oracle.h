@@ -91,6 +91,13 @@ int oqp_batch_solve(int B, int n, int m, const int *Pp, const int *Pi, const dou
                     const double *l_batch, const double *u_batch, const oqp_settings *s,
                     int nthreads, double *x_out, double *y_out, int *status_out, int *iter_out);
 
+/* Warm closed-loop step for B persistent solvers (the reference's per-step hot path:
+ * update(l, u) + update(Ax) + solve, src/trajectorySimulate.py:296,342,348), spread over
+ * `nthreads` threads.  Outputs x [B*n], status, iter (any may be NULL). */
+int oqp_batch_update_solve(int B, oqp_work **works, const double *Ax_batch, const double *l_batch,
+                           const double *u_batch, int nthreads, double *x_out, int *status_out,
+                           int *iter_out);
+
 #ifdef __cplusplus
 }
 #endif
