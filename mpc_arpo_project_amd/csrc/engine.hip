@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -57,7 +58,7 @@ struct DevPlan {
   const uint16_t *slotP, *slotA, *slotRho, *slotSig, *wsx, *wsz;
   const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
   int n, m, nk, nnzP, nnzA, nnzL;
-  int LX, DINV, W, ZERO, LDS_N, S_P, S_A, S_DT, S_ET;
+  int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
 };
 
 struct KParams {
@@ -235,7 +236,7 @@ __device__ __forceinline__ void run_dot2(const KParams& p, const StepHdr* hdr, i
     acc = group_sum(acc, glog, (int)((cur.mt >> META_GLOG_SHIFT) & 7u));
     if (cur.mt & META_HEAD) {
       const int t = (int)(cur.mt & META_TGT_MASK);
-      v[t] = v[t] - acc;
+      v[t] = (cur.mt & META_ZERO) ? -acc : v[t] - acc;
     }
     LDS_FENCE();
     cur = nxt;
@@ -263,6 +264,16 @@ __device__ __forceinline__ void load3(const DevPlan& P, const StepHdr& h, int la
     r.mt = in ? e : 0u;
 #pragma unroll
     for (int c = 0; c < MAXC3; ++c) r.t[c] = dummy;
+  } else if (kind == KIND_DOT2) {  // 2-factor terms (block inverses and couplings)
+    const uint32_t mt = P.meta[h.off_meta + li];
+    r.mt = in ? mt : 0u;
+    const uint64_t d2 = dummy & 0xffffffffu;
+#pragma unroll
+    for (int c = 0; c < MAXC3; ++c) {
+      const int cc = c < C ? c : 0;
+      const uint64_t t = P.terms2[h.off_terms + cc * cnt + li];
+      r.t[c] = (in && c < C) ? t : d2;
+    }
   } else {
     const uint32_t mt = P.meta[h.off_meta + li];
     r.mt = in ? mt : 0u;
@@ -290,6 +301,31 @@ __device__ __forceinline__ void run_factor(const KParams& p, double* v, int lane
       if (lane < (int)hc.cnt) {
         const int a = (int)(cur.mt & 0xffffu), d = (int)(cur.mt >> 16);
         v[a] = v[a] * v[d];
+      }
+    } else if (kind == KIND_DOT2) {
+      uint32_t t2[MAXC3];
+#pragma unroll
+      for (int c = 0; c < MAXC3; ++c) t2[c] = (uint32_t)cur.t[c];
+      double acc;
+      switch (C) {
+        case 0: acc = 0.0; break;
+        case 1: acc = dot2<1>(v, t2); break;
+        case 2: acc = dot2<2>(v, t2); break;
+        case 3: acc = dot2<3>(v, t2); break;
+        default: {
+          acc = dot2<4>(v, t2);
+          const int cnt = (int)hc.cnt, li = lane < cnt ? lane : 0;
+          for (int c = MAXC3; c < C; ++c) {
+            const uint32_t t = lane < cnt ? P.terms2[hc.off_terms + c * cnt + li]
+                                          : ((uint32_t)P.ZERO | ((uint32_t)P.ZERO << 16));
+            acc = fma(v[t & 0xffffu], v[t >> 16], acc);
+          }
+        }
+      }
+      acc = group_sum(acc, (int)((hc.cfg >> 8) & 0xffu), (int)((cur.mt >> META_GLOG_SHIFT) & 7u));
+      if (cur.mt & META_HEAD) {
+        const int t = (int)(cur.mt & META_TGT_MASK);
+        v[t] = (cur.mt & META_ZERO) ? -acc : v[t] - acc;
       }
     } else {
       double acc;
@@ -399,7 +435,11 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
   const DevPlan& P = p.pl;
   for (int k = lane; k < P.nnzL; k += 64) v[P.LX + k] = 0.0;
   for (int k = lane; k < P.nk; k += 64) v[P.W + k] = 0.0;
-  if (lane == 0) v[P.ZERO] = 0.0;
+  if (lane == 0) {
+    v[P.ZERO] = 0.0;
+    v[P.ONE] = 1.0;
+    v[P.MONE] = -1.0;
+  }
   LDS_FENCE();
   for (int j = lane; j < P.n; j += 64) v[P.slotSig[j]] = p.s.sigma;
   LDS_FENCE();
@@ -849,6 +889,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     const int i = lane + 64 * r;
     wsz[r] = i < m ? (int)P.wsz[i] : P.ZERO + 1;
   }
+  const int coff = P.CACC - P.W;  // rhs goes to the accumulator region, the solution comes back in W
   const double sigma = p.s.sigma, alpha = p.s.alpha;
   const int chk = p.s.check_termination;
   int ar_int = p.s.adaptive_rho_interval;
@@ -864,18 +905,18 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     for (int r = 0; r < RN; ++r) {
       const int j = lane + 64 * r;
       xp[r] = S.x[r];
-      if (j < n) v[wsx[r]] = sigma * xp[r] - S.q[r];
+      if (j < n) v[wsx[r] + coff] = sigma * xp[r] - S.q[r];
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       const int i = lane + 64 * r;
       zp[r] = S.z[r];
       bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
-      if (i < m) v[wsz[r]] = bz[r];
+      if (i < m) v[wsz[r] + coff] = bz[r];
     }
     LDS_FENCE();
     run_dot2(p, P.fwd, P.nfwd, tmeta, tterm, v, lane);
-    for (int k = lane; k < P.nk; k += 64) v[P.W + k] = v[P.W + k] * v[P.DINV + k];
+    for (int k = lane; k < P.nk; k += 64) v[P.CACC + k] = v[P.W + k] * v[P.DINV + k];
     LDS_FENCE();
     run_dot2(p, P.bwd, P.nbwd, tmeta, tterm, v, lane);
     // x, z, y updates (auxil.c update_x / update_z / update_y)
@@ -993,7 +1034,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 }
 
 // One workgroup = WPG <= 8 waves (blockDim.x = 64 * WPG); each wave solves its own instances.  The
-// workgroup's LDS holds one copy of the solve schedules followed by one instance image per wave.
+// workgroup's LDS holds one copy of the step headers followed by one instance image per wave.
 template <int RN, int RM>
 __global__ void __launch_bounds__(512) qp_batch_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1010,17 +1051,14 @@ __global__ void __launch_bounds__(512) qp_batch_kernel(KParams p) {
     for (int k = (int)threadIdx.x; k < hn[q]; k += (int)blockDim.x) tbl[off + k] = hsrc[q][k];
     off += hn[q];
   }
-  for (int k = (int)threadIdx.x; k < p.pl.nsmeta; k += (int)blockDim.x)
-    tbl[p.pl.hdr_words + k] = p.pl.smeta[k];
-  for (int k = (int)threadIdx.x; k < p.pl.nsterms; k += (int)blockDim.x)
-    tbl[p.pl.hdr_words + p.pl.nsmeta + k] = p.pl.sterms[k];
   __syncthreads();
   KParams q = p;  // schedule headers now read from the workgroup's LDS copy
   q.pl.fwd = reinterpret_cast<const StepHdr*>(tbl);
   q.pl.bwd = q.pl.fwd + p.pl.nfwd;
   q.pl.fac = q.pl.bwd + p.pl.nbwd;
-  const uint32_t* tmeta = tbl + p.pl.hdr_words;
-  const uint32_t* tterm = tmeta + p.pl.nsmeta;
+  // solve-step records stay in global memory (L2-resident, fetched one step ahead)
+  const uint32_t* tmeta = p.pl.smeta;
+  const uint32_t* tterm = p.pl.sterms;
   double* v = lds + p.pl.tbl_words / 2 + (size_t)wave * p.pl.inst_doubles;
   const size_t slab = (size_t)(p.pl.nnzP + p.pl.nnzA + 2 * p.pl.n + 2 * p.pl.m);
   double* scr = p.scratch + ((size_t)blockIdx.x * wpg + wave) * slab;
@@ -1048,6 +1086,14 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 typedef void (*kernel_fn)(KParams);
+
+// block caps of the blocked substitution (symbolic.hpp); MPCQP_CAPM / MPCQP_CAPW override them
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && *e) ? atoi(e) : dflt;
+}
+int cap_m() { return env_int("MPCQP_CAPM", 128); }
+int cap_w() { return env_int("MPCQP_CAPW", 384); }
 
 template <int RN, int RM>
 kernel_fn pick() {
@@ -1152,7 +1198,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   h->set = *s;
   h->B = batch;
   h->stream = (hipStream_t)stream;
-  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, MAXC, MAXC3, h->plan)) {
+  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, MAXC, MAXC3, h->plan, cap_m(),
+                  cap_w())) {
     std::string e = h->plan.error;
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, e);
@@ -1205,11 +1252,12 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   dp.smeta = (const uint32_t*)(b + o_sm), dp.sterms = (const uint32_t*)(b + o_st);
   dp.nsmeta = (int)pl.smeta.size(), dp.nsterms = (int)pl.sterms.size();
   dp.hdr_words = 4 * (dp.nfwd + dp.nbwd + dp.nfac);
-  dp.tbl_words = (dp.hdr_words + dp.nsmeta + dp.nsterms + 3) & ~3;
+  dp.tbl_words = (dp.hdr_words + 3) & ~3;
   dp.inst_doubles = (pl.LDS_N + 1) & ~1;
   dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
   dp.nnzL = pl.nnzL;
-  dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.ZERO = pl.ZERO, dp.LDS_N = pl.LDS_N;
+  dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.CACC = pl.CACC, dp.ZERO = pl.ZERO;
+  dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N;
   dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
 
   // occupancy -> workgroup size (waves sharing one LDS copy of the solve tables) and grid
@@ -1394,7 +1442,7 @@ int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t
                   int32_t* nnzL, int32_t* stats) {
   if (!st || !nnzL) return fail(MPCQP_E_INVALID, "null argument");
   Plan pl;
-  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, MAXC, MAXC3, pl))
+  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, MAXC, MAXC3, pl, cap_m(), cap_w()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   const int cap = *nnzL;
   *nnzL = pl.nnzL;

@@ -48,6 +48,7 @@ struct Task {
   uint32_t target;
   bool isD;
   std::vector<uint64_t> terms;  // packed a | b << 16 | c << 32
+  bool fromzero = false;
 };
 
 // Pack one level's tasks into 64-lane steps (see symbolic.hpp).
@@ -103,6 +104,7 @@ void pack_level(std::vector<Task>& tasks, StepKind kind, int max_c, int dummy_sl
         mt |= p->t->target & META_TGT_MASK;
         if (r == 0) mt |= META_HEAD;
         if (p->t->isD) mt |= META_ISD;
+        if (p->t->fromzero) mt |= META_ZERO;
         mrow[off + r] = mt;
       }
       const auto& tv = p->t->terms;
@@ -139,7 +141,7 @@ void pack_scale(const std::vector<uint32_t>& entries, std::vector<StepHdr>& step
 }  // namespace
 
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, int max_c, int max_c3, Plan& pl) {
+                const int32_t* Ai, int max_c, int max_c3, Plan& pl, int capM, int capW) {
   pl = Plan();
   pl.n = n, pl.m = m, pl.nk = n + m;
   const int nk = n + m;
@@ -238,19 +240,127 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     return (it != e && *it == i) ? (int)(it - pl.Li.begin()) : -1;
   };
 
+  // ---- blocked substitution (see symbolic.hpp): contiguous blocks of the permuted order,
+  // chosen greedily; reach(r) = rows of r's block that r depends on (transitively)
+  std::vector<std::vector<int>> reach(nk);
+  std::vector<int> blk(nk, 0);
+  pl.block_start.clear();
+  {
+    int a = 0;
+    while (a < nk) {
+      int pa = pl.block_start.empty() ? 0 : pl.block_start.back();
+      int pb = a;  // previous block [pa, pb)
+      long msz = 0, wterms = 0;
+      int b = a;
+      while (b < nk) {
+        // reach of row b restricted to [a, b)
+        std::vector<int> rs;
+        for (int k : lrow[b])
+          if (k >= a) {
+            rs.push_back(k);
+            rs.insert(rs.end(), reach[k].begin(), reach[k].end());
+          }
+        std::sort(rs.begin(), rs.end());
+        rs.erase(std::unique(rs.begin(), rs.end()), rs.end());
+        // G pattern of row b: deps of {b} U reach(b) inside the previous block
+        std::vector<int> gp;
+        for (int r2 : rs)
+          for (int x : lrow[r2])
+            if (x >= pa && x < pb) gp.push_back(x);
+        for (int x : lrow[b])
+          if (x >= pa && x < pb) gp.push_back(x);
+        std::sort(gp.begin(), gp.end());
+        gp.erase(std::unique(gp.begin(), gp.end()), gp.end());
+        long nm = msz + (long)rs.size(), nw = wterms + (long)rs.size() + 1 + (long)gp.size();
+        if (b > a && (nm > capM || nw > capW)) break;
+        reach[b] = std::move(rs);
+        msz = nm, wterms = nw;
+        b++;
+      }
+      pl.block_start.push_back(a);
+      for (int r = a; r < b; r++) blk[r] = (int)pl.block_start.size() - 1;
+      a = b;
+    }
+    pl.block_start.push_back(nk);
+  }
+  const int T = (int)pl.block_start.size() - 1;
+  auto bs = [&](int k) { return pl.block_start[k]; };
+  auto be = [&](int k) { return pl.block_start[k + 1]; };
+  // transposed reach: rtr[r] = rows r' of r's block with r in reach(r')
+  std::vector<std::vector<int>> rtr(nk);
+  for (int r = 0; r < nk; r++)
+    for (int r2 : reach[r]) rtr[r2].push_back(r);
+  // G pattern (previous block) and G' pattern (next block) per row
+  std::vector<std::vector<int>> gpat(nk), gppat(nk);
+  for (int r = 0; r < nk; r++) {
+    const int k = blk[r];
+    if (k > 0) {
+      std::vector<int> g;
+      auto add = [&](int rr) {
+        for (int x : lrow[rr])
+          if (x >= bs(k - 1) && x < be(k - 1)) g.push_back(x);
+      };
+      add(r);
+      for (int rr : reach[r]) add(rr);
+      std::sort(g.begin(), g.end());
+      g.erase(std::unique(g.begin(), g.end()), g.end());
+      gpat[r] = std::move(g);
+    }
+    if (k + 1 < T) {
+      std::vector<int> g;
+      auto add = [&](int rr) {  // z in next block with L_{z, rr} != 0
+        for (int z : lcol[rr])
+          if (z >= bs(k + 1) && z < be(k + 1)) g.push_back(z);
+      };
+      add(r);
+      for (int rr : rtr[r]) add(rr);
+      std::sort(g.begin(), g.end());
+      g.erase(std::unique(g.begin(), g.end()), g.end());
+      gppat[r] = std::move(g);
+    }
+  }
   // ---- LDS layout (doubles)
   pl.LX = 0;
   pl.DINV = pl.nnzL;
   pl.W = pl.DINV + nk;
-  pl.ZERO = pl.W + nk;
-  pl.LDS_N = pl.ZERO + 2;  // +1 pad keeps the total even
+  pl.CACC = pl.W + nk;
+  pl.NB = pl.CACC + nk;
+  std::vector<int> noff(nk + 1, 0), goff(nk + 1, 0), gpoff(nk + 1, 0);
+  for (int r = 0; r < nk; r++) {
+    noff[r + 1] = noff[r] + (int)reach[r].size();
+    goff[r + 1] = goff[r] + (int)gpat[r].size();
+    gpoff[r + 1] = gpoff[r] + (int)gppat[r].size();
+  }
+  pl.nN = noff[nk], pl.nG = goff[nk], pl.nGP = gpoff[nk];
+  pl.GB = pl.NB + pl.nN;
+  pl.GPB = pl.GB + pl.nG;
+  pl.ZERO = pl.GPB + pl.nGP;
+  pl.ONE = pl.ZERO + 1;
+  pl.MONE = pl.ZERO + 2;
+  pl.LDS_N = pl.ZERO + 4;  // keeps the image a multiple of 16 bytes with an even base
+  // slot of N_{r r2} (r2 in reach(r) or r2 == r -> MONE), G_{r x}, G'_{r z}
+  auto nslot = [&](int r, int r2) -> int {
+    if (r2 == r) return pl.MONE;
+    auto it = std::lower_bound(reach[r].begin(), reach[r].end(), r2);
+    if (it == reach[r].end() || *it != r2) return -1;
+    return pl.NB + noff[r] + (int)(it - reach[r].begin());
+  };
+  auto gslot = [&](int r, int x) {
+    auto it = std::lower_bound(gpat[r].begin(), gpat[r].end(), x);
+    return pl.GB + goff[r] + (int)(it - gpat[r].begin());
+  };
+  auto gpslot = [&](int r, int z) {
+    auto it = std::lower_bound(gppat[r].begin(), gppat[r].end(), z);
+    return pl.GPB + gpoff[r] + (int)(it - gppat[r].begin());
+  };
   // scaling overlay
   pl.S_P = 0;
   pl.S_A = pl.S_P + pl.nnzP;
   pl.S_DT = pl.S_A + pl.nnzA;
   pl.S_ET = pl.S_DT + n;
   if (pl.S_ET + m > pl.LDS_N) pl.LDS_N = pl.S_ET + m;
-  // the residual SpMVs stage x (n) and y (m) as plain arrays in the W region: W + [0, n + m)
+  pl.LDS_N = (pl.LDS_N + 1) & ~1;
+  // the residual SpMVs stage x (n) and y (m) as plain arrays in the W + C regions
   if (pl.LDS_N >= 65535) {
     pl.error = "LDS image too large for 16-bit slots";
     return false;
@@ -301,8 +411,6 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     for (int i : lcol[j]) blev[j] = std::max(blev[j], blev[i] + 1);
   int maxlev = *std::max_element(lev.begin(), lev.end());
   int maxblev = *std::max_element(blev.begin(), blev.end());
-  pl.levels_fwd = maxlev + 1;
-  pl.levels_bwd = maxblev + 1;
   std::vector<std::vector<int>> bylev(maxlev + 1), byblev(maxblev + 1);
   for (int i = 0; i < nk; i++) bylev[lev[i]].push_back(i), byblev[blev[i]].push_back(i);
 
@@ -351,30 +459,123 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     pack_level(tasks, KIND_DOT3, max_c3, Z, pl.fac, pl.meta, pl.terms2, pl.terms3);
     pack_scale(scal, pl.fac, pl.terms2);
   }
-  // ---- forward solve L w = b
-  for (int L = 1; L <= maxlev; L++) {
+  // ---- factorization tail: N (negated block inverses), then G and G' (one level)
+  {
+    // N_{r r2} = -sum_{t in lrow(r), r2 <= t < r} L_{rt} N_{t r2}   (N_{tt} = -1), by depth in block
+    std::vector<int> depth(nk, 0);
+    int maxd = 0;
+    for (int r = 0; r < nk; r++) {
+      for (int k : lrow[r])
+        if (k >= bs(blk[r])) depth[r] = std::max(depth[r], depth[k] + 1);
+      maxd = std::max(maxd, depth[r]);
+    }
+    for (int dl = 1; dl <= maxd; dl++) {
+      std::vector<Task> tasks;
+      for (int r = 0; r < nk; r++) {
+        if (depth[r] != dl) continue;
+        for (int r2 : reach[r]) {
+          Task t;
+          t.target = (uint32_t)nslot(r, r2);
+          t.isD = false;
+          t.fromzero = true;
+          for (int tt : lrow[r]) {
+            if (tt < r2) continue;
+            int ns = nslot(tt, r2);
+            if (ns < 0) continue;
+            t.terms.push_back(T2(pl.LX + lpos(r, tt), ns));
+          }
+          tasks.push_back(std::move(t));
+        }
+      }
+      pack_level(tasks, KIND_DOT2, max_c3, Z, pl.fac, pl.meta, pl.terms2, pl.terms3);
+    }
     std::vector<Task> tasks;
-    for (int i : bylev[L]) {
+    for (int r = 0; r < nk; r++) {
+      // G_{r x} = -sum_{r2 in reach(r) U {r}} N_{r r2} L_{r2 x}
+      for (int x : gpat[r]) {
+        Task t;
+        t.target = (uint32_t)gslot(r, x);
+        t.isD = false;
+        t.fromzero = true;
+        std::vector<int> src(reach[r].begin(), reach[r].end());
+        src.push_back(r);
+        for (int r2 : src) {
+          int p = lpos(r2, x);
+          if (p >= 0) t.terms.push_back(T2(nslot(r, r2), pl.LX + p));
+        }
+        tasks.push_back(std::move(t));
+      }
+      // G'_{r z} = -sum_{r2: r in reach(r2) or r2 == r} N_{r2 r} L_{z r2}
+      for (int z : gppat[r]) {
+        Task t;
+        t.target = (uint32_t)gpslot(r, z);
+        t.isD = false;
+        t.fromzero = true;
+        std::vector<int> src(rtr[r].begin(), rtr[r].end());
+        src.push_back(r);
+        for (int r2 : src) {
+          int p = lpos(z, r2);
+          if (p >= 0) t.terms.push_back(T2(nslot(r2, r), pl.LX + p));
+        }
+        tasks.push_back(std::move(t));
+      }
+    }
+    pack_level(tasks, KIND_DOT2, max_c3, Z, pl.fac, pl.meta, pl.terms2, pl.terms3);
+  }
+  // ---- forward solve (input C = rhs, output W): per block k
+  //   W_r = sum_{r2 in reach(r) U {r}} M_{r r2} C_{r2} - sum_{x in block k-1} G_{r x} W_x
+  //   C_r -= sum_{x in block k-1} L_{r x} W_x          for rows r beyond block k
+  for (int k = 0; k < T; k++) {
+    std::vector<Task> tasks;
+    for (int r = bs(k); r < be(k); r++) {
       Task t;
-      t.target = (uint32_t)(pl.W + i);
+      t.target = (uint32_t)(pl.W + r);
       t.isD = false;
-      for (int k : lrow[i]) t.terms.push_back(T2(pl.LX + lpos(i, k), pl.W + k));
+      t.fromzero = true;
+      for (int r2 : reach[r]) t.terms.push_back(T2(nslot(r, r2), pl.CACC + r2));
+      t.terms.push_back(T2(pl.MONE, pl.CACC + r));
+      for (int x : gpat[r]) t.terms.push_back(T2(gslot(r, x), pl.W + x));
       tasks.push_back(std::move(t));
     }
+    if (k >= 1)
+      for (int r = be(k); r < nk; r++) {
+        Task t;
+        t.target = (uint32_t)(pl.CACC + r);
+        t.isD = false;
+        for (int x : lrow[r])
+          if (x >= bs(k - 1) && x < be(k - 1)) t.terms.push_back(T2(pl.LX + lpos(r, x), pl.W + x));
+        if (!t.terms.empty()) tasks.push_back(std::move(t));
+      }
     pack_level(tasks, KIND_DOT2, max_c, Z, pl.fwd, pl.smeta, pl.sterms, pl.terms3);
   }
-  // ---- backward solve L' x = w
-  for (int L = 1; L <= maxblev; L++) {
+  // ---- backward solve (input C = D^-1 W, output W): blocks in reverse
+  //   W_r = sum_{r2: r in reach(r2) or r2 == r} M_{r2 r} C_{r2} - sum_{z in block k+1} G'_{r z} W_z
+  //   C_r -= sum_{z in block k+1} L_{z r} W_z          for rows r before block k
+  for (int k = T - 1; k >= 0; k--) {
     std::vector<Task> tasks;
-    for (int j : byblev[L]) {
+    for (int r = bs(k); r < be(k); r++) {
       Task t;
-      t.target = (uint32_t)(pl.W + j);
+      t.target = (uint32_t)(pl.W + r);
       t.isD = false;
-      for (int i : lcol[j]) t.terms.push_back(T2(pl.LX + lpos(i, j), pl.W + i));
+      t.fromzero = true;
+      for (int r2 : rtr[r]) t.terms.push_back(T2(nslot(r2, r), pl.CACC + r2));
+      t.terms.push_back(T2(pl.MONE, pl.CACC + r));
+      for (int z : gppat[r]) t.terms.push_back(T2(gpslot(r, z), pl.W + z));
       tasks.push_back(std::move(t));
     }
+    if (k + 1 < T)
+      for (int r = 0; r < bs(k); r++) {
+        Task t;
+        t.target = (uint32_t)(pl.CACC + r);
+        t.isD = false;
+        for (int z : lcol[r])
+          if (z >= bs(k + 1) && z < be(k + 1)) t.terms.push_back(T2(pl.LX + lpos(z, r), pl.W + z));
+        if (!t.terms.empty()) tasks.push_back(std::move(t));
+      }
     pack_level(tasks, KIND_DOT2, max_c, Z, pl.bwd, pl.smeta, pl.sterms, pl.terms3);
   }
+  pl.levels_fwd = T;
+  pl.levels_bwd = T;
 
   // ---- matrix structure for scaling / residuals
   pl.Ap.resize(n + 1);

@@ -36,13 +36,19 @@ constexpr uint32_t META_TGT_MASK = 0xffffu;
 constexpr int META_GLOG_SHIFT = 16;  // 3 bits: this lane's group size log2
 constexpr uint32_t META_HEAD = 1u << 19;
 constexpr uint32_t META_ISD = 1u << 20;  // factorization: target is D_j -> also write 1/D_j
+constexpr uint32_t META_ZERO = 1u << 21; // v[t] <- -sum (instead of v[t] - sum)
 constexpr uint32_t META_ACTIVE = 1u << 31;
 
 struct Plan {
   int n = 0, m = 0, nk = 0, nnzP = 0, nnzA = 0, nnzL = 0;
   std::vector<int32_t> perm, pinv, Lp, Li, etree;
-  // LDS layout, in doubles
-  int LX = 0, DINV = 0, W = 0, ZERO = 0, LDS_N = 0;
+  // LDS layout, in doubles: L | 1/D | W (solve vector) | C (accumulators) | N (negated block
+  // inverses) | G | G' | ZERO ONE MONE pad
+  int LX = 0, DINV = 0, W = 0, CACC = 0, NB = 0, GB = 0, GPB = 0, ZERO = 0, ONE = 0, MONE = 0;
+  int LDS_N = 0;
+  // blocked substitution: contiguous blocks of the permuted order
+  std::vector<int32_t> block_start;  // T + 1 entries
+  int nN = 0, nG = 0, nGP = 0;
   // scaling-phase overlay of the same LDS: scaled P, scaled A, D_temp, E_temp
   int S_P = 0, S_A = 0, S_DT = 0, S_ET = 0;
   // KKT assembly: LDS slot of each P entry (diagonal -> D slot), A entry, rho diagonal,
@@ -69,7 +75,9 @@ struct Plan {
 // Builds the plan; returns false (with plan.error set) if the structure is unsupported.
 // max_c / max_c3: max terms per lane per solve / factorization step before a task is widened to
 // more lanes.
+// capM / capW: per block, max entries of the block inverse and max solve terms of its w-tasks.
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, int max_c, int max_c3, Plan& plan);
+                const int32_t* Ai, int max_c, int max_c3, Plan& plan, int capM = 128,
+                int capW = 384);
 
 }  // namespace mpcqp
