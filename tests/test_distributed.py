@@ -1,0 +1,61 @@
+"""Multi-rank plumbing of the sharded workload on CPU (gloo, world_size 2): every rank builds its
+contiguous shard of chasers from the global seed, computes its per-step QP data, and the final
+all-gather reproduces the single-process batch exactly (what bench.py relies on for N > 1)."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, B, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from conftest import problem
+    from mpc_arpo_project_amd import qp_model
+
+    prob = problem(20, False)
+    X = bench.initial_states(world * B, rank, B, 20250328)
+    xest = np.hstack([X, np.zeros((B, 2))])
+    Ax, l, u = qp_model.configure_batch(prob, xest)
+    t = torch.as_tensor(np.hstack([Ax, l, u]))
+    g = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(g, t)
+    if rank == 0:
+        torch.save(torch.cat(g), out_path)
+    dist.destroy_process_group()
+
+
+def test_sharded_gather_matches_single_process(tmp_path):
+    world, B = 2, 16
+    out = str(tmp_path / "gathered.pt")
+    mp.spawn(_worker, args=(world, _free_port(), B, out), nprocs=world, join=True)
+    gathered = torch.load(out, weights_only=True).numpy()
+    import bench
+    from conftest import problem
+    from mpc_arpo_project_amd import qp_model
+
+    prob = problem(20, False)
+    X = bench.initial_states(world * B, 0, world * B, 20250328)
+    Ax, l, u = qp_model.configure_batch(prob, np.hstack([X, np.zeros((world * B, 2))]))
+    assert np.array_equal(gathered, np.hstack([Ax, l, u]))
+
+
+def test_shard_ranges_cover_batch():
+    import bench
+
+    world, B = 4, 8
+    parts = [bench.initial_states(world * B, r, B, 7) for r in range(world)]
+    full = bench.initial_states(world * B, 0, world * B, 7)
+    assert np.array_equal(np.vstack(parts), full)
