@@ -79,9 +79,7 @@ def cpu_baseline(prob, X0, steps, warmup, eps, sample, threads, device):
     t_cpu = 0.0
     for k in range(warmup + steps):
         if k == 0:
-            for s in solvers:
-                s._last = s.solve()
-            st = np.array([s._last.info.status_val for s in solvers])
+            _, st, _ = orc.batch_update_solve(solvers, None, None, None, threads)
         else:
             t0 = time.perf_counter()
             _, st, _ = orc.batch_update_solve(solvers, rec[k][0], rec[k][1], rec[k][2], threads)
@@ -106,7 +104,7 @@ def main():
     ap.add_argument("--nx", type=int, default=20)
     ap.add_argument("--eps", type=float, default=1e-4)
     ap.add_argument("--seed", type=int, default=20250328)
-    ap.add_argument("--cpu-sample", type=int, default=512)
+    ap.add_argument("--cpu-sample", type=int, default=8192)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -40,21 +40,12 @@ using namespace mpcqp;
 
 namespace {
 
-constexpr int MAXC = 8;  // terms per lane kept in the prefetch registers
-
 // ------------------------------------------------------------------------------------- device
 struct DevPlan {
-  const StepHdr *fac, *fwd, *bwd;
-  int nfac, nfwd, nbwd;
-  const uint32_t* meta;    // factorization pools (global)
-  const uint32_t* terms2;
-  const uint64_t* terms3;
-  const uint32_t* smeta;   // solve pools: global source of the per-workgroup LDS copy
-  const uint32_t* sterms;
-  int nsmeta, nsterms;     // words
-  int hdr_words;           // fwd + bwd + fac step headers, copied to the front of the table region
-  int tbl_words;           // LDS words of the table region (16-byte aligned)
-  int inst_doubles;        // LDS doubles per instance image (16-byte aligned)
+  const uint32_t *fac, *tail, *fwd, *bwd;  // fixed-stride step records (symbolic.hpp)
+  int nfac, ntail, nfwd, nbwd;
+  const uint16_t* Lcol;    // DINV slot of each L entry's column
+  int inst_doubles;        // LDS doubles of the instance image (16-byte aligned)
   const uint16_t *slotP, *slotA, *slotRho, *slotSig, *wsx, *wsz;
   const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
   int n, m, nk, nnzP, nnzA, nnzL;
@@ -102,46 +93,82 @@ __device__ __forceinline__ double limit_scaling(double d) {
 }
 
 // ---- level-scheduled dot-product steps (see symbolic.hpp) ---------------------------------
-// Step headers live in the workgroup's LDS table region (copied at kernel start).
-__device__ __forceinline__ StepHdr ld_hdr(const StepHdr* p, int s) { return p[s]; }
+// The instance image starts at LDS address 0 (one wave per workgroup, no static LDS), so the
+// schedule records hold absolute LDS byte addresses and an operand fetch is a bare ds_read.
+typedef __attribute__((address_space(3))) double lds_double;
+__device__ __forceinline__ double lds_ld(const double*, uint32_t a) {
+  return *(const lds_double*)(size_t)a;
+}
+__device__ __forceinline__ void lds_st(double*, uint32_t a, double x) { *(lds_double*)(size_t)a = x; }
 
 // 64-bit cross-lane moves for the group butterflies: DPP inside rows of 16 lanes (quad_perm xor 1,
 // xor 2, row_half_mirror, row_mirror pair the partners of an aligned group exactly like an xor
 // butterfly does for an all-reduce), ds_bpermute beyond that.
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, false);
   return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double group_partner(double x, int k) {
-  switch (k) {
-    case 0: return dpp_d<0xB1>(x);   // quad_perm [1,0,3,2]
-    case 1: return dpp_d<0x4E>(x);   // quad_perm [2,3,0,1]
-    case 2: return dpp_d<0x141>(x);  // row_half_mirror
-    case 3: return dpp_d<0x140>(x);  // row_mirror
-    default: return __shfl_xor(x, 1 << k);
-  }
-}
-// all-reduce of acc over this lane's aligned group of 2^gl lanes (glog = max over the step)
-__device__ __forceinline__ double group_sum(double acc, int glog, int gl) {
-  for (int k = 0; k < glog; ++k) {
-    const double o = group_partner(acc, k);
-    if (k < gl) acc += o;
+// all-reduce of acc over this lane's aligned group of 2^gl lanes (glog = widest group of the step,
+// wave-uniform)
+__device__ __forceinline__ double group_sum(double acc, uint32_t glog, uint32_t gl) {
+  if (glog > 0) {
+    const double o = dpp_d<0xB1>(acc);  // quad_perm [1,0,3,2]
+    if (gl > 0) acc += o;
+    if (glog > 1) {
+      const double o2 = dpp_d<0x4E>(acc);  // quad_perm [2,3,0,1]
+      if (gl > 1) acc += o2;
+      if (glog > 2) {
+        const double o3 = dpp_d<0x141>(acc);  // row_half_mirror
+        if (gl > 2) acc += o3;
+        if (glog > 3) {
+          const double o4 = dpp_d<0x140>(acc);  // row_mirror
+          if (gl > 3) acc += o4;
+          for (uint32_t k = 4; k < glog; ++k) {
+            const double o5 = __shfl_xor(acc, 1 << k);
+            if (gl > k) acc += o5;
+          }
+        }
+      }
+    }
   }
   return acc;
 }
 
-// straight-line dot products (two accumulators to halve the dependent FMA chain)
-// All 2C LDS reads are forced in front of the FMAs (sched_group_barrier: 0x100 = DS read,
-// 0x002 = VALU) so that they overlap instead of paying one LDS round trip per term.
+// one lane's records of a solve step: meta word + SOLVE_MAXC (a, b) address pairs
+struct SolveRec {
+  uint32_t mt;
+  uint2 t[SOLVE_MAXC];
+};
+__device__ __forceinline__ void load_solve(const uint32_t* step, int lane, SolveRec& r) {
+  r.mt = step[lane];
+  const uint2* tp = reinterpret_cast<const uint2*>(step + 64) + lane;
+#pragma unroll
+  for (int c = 0; c < SOLVE_MAXC; ++c) r.t[c] = tp[c * 64];
+}
+// one lane's records of a factorization step: meta word + FAC_MAXC (a, b, c, -) address quads
+struct FacRec {
+  uint32_t mt;
+  uint4 t[FAC_MAXC];
+};
+__device__ __forceinline__ void load_fac(const uint32_t* step, int lane, FacRec& r) {
+  r.mt = step[lane];
+  const uint4* tp = reinterpret_cast<const uint4*>(step + 64) + lane;
+#pragma unroll
+  for (int c = 0; c < FAC_MAXC; ++c) r.t[c] = tp[c * 64];
+}
+
+// straight-line dot products (two accumulators halve the dependent FMA chain).  All LDS reads are
+// forced in front of the FMAs (sched_group_barrier: 0x100 = DS read, 0x002 = VALU) so that they
+// overlap instead of paying one LDS round trip per term.
 template <int C>
-__device__ __forceinline__ double dot2(const double* v, const uint32_t* t) {
+__device__ __forceinline__ double dot2(const double* v, const uint2* t) {
   double x[C], y[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    x[c] = v[t[c] & 0xffffu];
-    y[c] = v[t[c] >> 16];
+    x[c] = lds_ld(v, t[c].x);
+    y[c] = lds_ld(v, t[c].y);
   }
   __builtin_amdgcn_sched_group_barrier(0x100, 2 * C, 0);
   __builtin_amdgcn_sched_group_barrier(0x002, 2 * C, 0);
@@ -156,13 +183,13 @@ __device__ __forceinline__ double dot2(const double* v, const uint32_t* t) {
   return a0 + a1;
 }
 template <int C>
-__device__ __forceinline__ double dot3(const double* v, const uint64_t* t) {
+__device__ __forceinline__ double dot3(const double* v, const uint4* t) {
   double x[C], y[C], d[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    x[c] = v[t[c] & 0xffffu];
-    y[c] = v[(t[c] >> 16) & 0xffffu];
-    d[c] = v[t[c] >> 32];
+    x[c] = lds_ld(v, t[c].x);
+    y[c] = lds_ld(v, t[c].y);
+    d[c] = lds_ld(v, t[c].z);
   }
   __builtin_amdgcn_sched_group_barrier(0x100, 3 * C, 0);
   __builtin_amdgcn_sched_group_barrier(0x002, 3 * C, 0);
@@ -177,185 +204,85 @@ __device__ __forceinline__ double dot3(const double* v, const uint64_t* t) {
   return a0 + a1;
 }
 
-struct Pref2 {
-  uint32_t mt;
-  uint32_t t[MAXC];
-};
-
-// branch-free fetch of one solve step's lane records from the workgroup's LDS tables: lanes past
-// cnt and terms past C read a clamped (valid) address and are replaced by the dummy record
-__device__ __forceinline__ void load2(const StepHdr& h, const uint32_t* tmeta,
-                                      const uint32_t* tterm, int lane, uint32_t dummy, Pref2& r) {
-  const int C = (int)(h.cfg & 0xffu), cnt = (int)h.cnt;
-  const bool in = lane < cnt;
-  const int li = in ? lane : 0;
-  const uint32_t mt = tmeta[h.off_meta + li];
-  r.mt = in ? mt : 0u;
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    const int cc = c < C ? c : 0;
-    const uint32_t t = tterm[h.off_terms + cc * cnt + li];
-    r.t[c] = (in && c < C) ? t : dummy;
+// One solve step: v[t] <- -sum_c v[a_c] * v[b_c].  Every lane stores: the lanes of a group hold
+// the group's bitwise-identical sum and store it to the task's slot, idle lanes store to their
+// own sink slot, so the store needs no branch.
+__device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(r.mt);
+  const uint32_t C = (m0 >> META_C_SHIFT) & 15u, glog = (m0 >> META_SGLOG_SHIFT) & 7u;
+  double acc;
+  if (C <= 2)
+    acc = dot2<2>(v, r.t);
+  else if (C <= 4)
+    acc = dot2<4>(v, r.t);
+  else
+    acc = dot2<8>(v, r.t);
+  acc = group_sum(acc, glog, (r.mt >> META_GLOG_SHIFT) & 7u);
+  lds_st(v, r.mt & META_TGT_MASK, -acc);
+  LDS_FENCE();
+}
+// One factorization step: v[t] <- -sum_c v[a_c] v[b_c] v[c_c]; a D_j target also writes 1/D_j at
+// byte offset dshift from it.  Only group heads store (idle lanes have no slot).
+__device__ __forceinline__ void fac_step(const FacRec& r, double* v, uint32_t dshift) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(r.mt);
+  const uint32_t C = (m0 >> META_C_SHIFT) & 15u, glog = (m0 >> META_SGLOG_SHIFT) & 7u;
+  double acc = C <= 2 ? dot3<2>(v, r.t) : dot3<4>(v, r.t);
+  acc = group_sum(acc, glog, (r.mt >> META_GLOG_SHIFT) & 7u);
+  if (r.mt & META_HEAD) {
+    const uint32_t t = r.mt & META_TGT_MASK;
+    const double nv = -acc;
+    lds_st(v, t, nv);
+    if (r.mt & META_ISD) lds_st(v, t + dshift, 1.0 / nv);
   }
+  LDS_FENCE();
 }
 
-// forward / backward triangular solve: v[t] <- v[t] - sum_c v[a_c] * v[b_c]
-__device__ __forceinline__ void run_dot2(const KParams& p, const StepHdr* hdr, int nsteps,
-                                         const uint32_t* tmeta, const uint32_t* tterm, double* v,
-                                         int lane) {
-  if (nsteps <= 0) return;
-  const uint32_t dummy = (uint32_t)p.pl.ZERO | ((uint32_t)p.pl.ZERO << 16);
-  Pref2 cur, nxt;
-  StepHdr hc = ld_hdr(hdr, 0);
-  StepHdr hn = ld_hdr(hdr, nsteps > 1 ? 1 : 0);
-  load2(hc, tmeta, tterm, lane, dummy, cur);
-  for (int s = 0; s < nsteps; ++s) {
-    // records of step s+1 (header already in registers) and header of step s+2
-    load2(hn, tmeta, tterm, lane, dummy, nxt);
-    const StepHdr hn2 = ld_hdr(hdr, s + 2 < nsteps ? s + 2 : 0);
-    const int C = (int)(hc.cfg & 0xffu), glog = (int)((hc.cfg >> 8) & 0xffu);
-    double acc;
-    switch (C) {
-      case 0: acc = 0.0; break;
-      case 1: acc = dot2<1>(v, cur.t); break;
-      case 2: acc = dot2<2>(v, cur.t); break;
-      case 3: acc = dot2<3>(v, cur.t); break;
-      case 4: acc = dot2<4>(v, cur.t); break;
-      case 5: acc = dot2<5>(v, cur.t); break;
-      case 6: acc = dot2<6>(v, cur.t); break;
-      case 7: acc = dot2<7>(v, cur.t); break;
-      default: {
-        acc = dot2<8>(v, cur.t);
-        const int cnt = (int)hc.cnt, li = lane < cnt ? lane : 0;
-        for (int c = MAXC; c < C; ++c) {  // very long rows only
-          const uint32_t t = lane < cnt ? tterm[hc.off_terms + c * cnt + li] : dummy;
-          acc = fma(v[t & 0xffffu], v[t >> 16], acc);
-        }
-      }
-    }
-    acc = group_sum(acc, glog, (int)((cur.mt >> META_GLOG_SHIFT) & 7u));
-    if (cur.mt & META_HEAD) {
-      const int t = (int)(cur.mt & META_TGT_MASK);
-      v[t] = (cur.mt & META_ZERO) ? -acc : v[t] - acc;
-    }
-    LDS_FENCE();
-    cur = nxt;
-    hc = hn;
-    hn = hn2;
+// Step loops.  Records (L2-resident, fixed stride) rotate through three register sets, so the
+// records of step s + 2 are in flight while steps s and s + 1 compute.
+template <typename Rec, typename Load, typename Step>
+__device__ __forceinline__ void run_steps(const uint32_t* tbl, int n, int lane, Load load, Step step) {
+  if (n <= 0) return;
+  auto at = [&](int s) { return tbl + (size_t)(s < n ? s : n - 1) * STEP_WORDS; };
+  Rec a, b, c;
+  load(at(0), lane, a);
+  load(at(1), lane, b);
+  load(at(2), lane, c);
+  int s = 0;
+  for (;;) {
+    step(a);
+    if (++s >= n) break;
+    load(at(s + 2), lane, a);
+    step(b);
+    if (++s >= n) break;
+    load(at(s + 2), lane, b);
+    step(c);
+    if (++s >= n) break;
+    load(at(s + 2), lane, c);
   }
 }
-
-// numeric LDL' factorization (left-looking, dot-product form) + per-level scaling L_ij *= 1/D_j.
-// Records come from global memory (L2-resident); the next step's records are fetched while the
-// current step computes.
-constexpr int MAXC3 = 4;
-struct Pref3 {
-  uint32_t mt;
-  uint64_t t[MAXC3];
-};
-
-__device__ __forceinline__ void load3(const DevPlan& P, const StepHdr& h, int lane, uint64_t dummy,
-                                      Pref3& r) {
-  const int kind = (int)(h.cfg >> 16), C = (int)(h.cfg & 0xffu), cnt = (int)h.cnt;
-  const bool in = lane < cnt;
-  const int li = in ? lane : 0;
-  if (kind == KIND_SCALE) {
-    const uint32_t e = P.terms2[h.off_terms + li];
-    r.mt = in ? e : 0u;
-#pragma unroll
-    for (int c = 0; c < MAXC3; ++c) r.t[c] = dummy;
-  } else if (kind == KIND_DOT2) {  // 2-factor terms (block inverses and couplings)
-    const uint32_t mt = P.meta[h.off_meta + li];
-    r.mt = in ? mt : 0u;
-    const uint64_t d2 = dummy & 0xffffffffu;
-#pragma unroll
-    for (int c = 0; c < MAXC3; ++c) {
-      const int cc = c < C ? c : 0;
-      const uint64_t t = P.terms2[h.off_terms + cc * cnt + li];
-      r.t[c] = (in && c < C) ? t : d2;
-    }
-  } else {
-    const uint32_t mt = P.meta[h.off_meta + li];
-    r.mt = in ? mt : 0u;
-#pragma unroll
-    for (int c = 0; c < MAXC3; ++c) {
-      const int cc = c < C ? c : 0;
-      const uint64_t t = P.terms3[h.off_terms + (size_t)cc * cnt + li];
-      r.t[c] = (in && c < C) ? t : dummy;
-    }
-  }
+__device__ __forceinline__ void run_solve(const uint32_t* tbl, int nsteps, double* v, int lane) {
+  run_steps<SolveRec>(
+      tbl, nsteps, lane,
+      [](const uint32_t* st, int ln, SolveRec& r) { load_solve(st, ln, r); },
+      [v](const SolveRec& r) { solve_step(r, v); });
+}
+__device__ __forceinline__ void run_fac(const uint32_t* tbl, int nsteps, double* v, int lane,
+                                        uint32_t dshift) {
+  run_steps<FacRec>(
+      tbl, nsteps, lane, [](const uint32_t* st, int ln, FacRec& r) { load_fac(st, ln, r); },
+      [v, dshift](const FacRec& r) { fac_step(r, v, dshift); });
 }
 
+// numeric LDL': U = L D and D by levels, L = U / D (flat pass), then the block-inverse tail
 __device__ __forceinline__ void run_factor(const KParams& p, double* v, int lane) {
   const DevPlan& P = p.pl;
-  if (P.nfac <= 0) return;
-  const uint64_t dummy3 = (uint64_t)P.ZERO | ((uint64_t)P.ZERO << 16) | ((uint64_t)P.ZERO << 32);
-  Pref3 cur, nxt;
-  StepHdr hc = ld_hdr(P.fac, 0);
-  load3(P, hc, lane, dummy3, cur);
-  for (int s = 0; s < P.nfac; ++s) {
-    const StepHdr hn = ld_hdr(P.fac, s + 1 < P.nfac ? s + 1 : 0);
-    load3(P, hn, lane, dummy3, nxt);
-    const int kind = (int)(hc.cfg >> 16), C = (int)(hc.cfg & 0xffu);
-    if (kind == KIND_SCALE) {
-      if (lane < (int)hc.cnt) {
-        const int a = (int)(cur.mt & 0xffffu), d = (int)(cur.mt >> 16);
-        v[a] = v[a] * v[d];
-      }
-    } else if (kind == KIND_DOT2) {
-      uint32_t t2[MAXC3];
-#pragma unroll
-      for (int c = 0; c < MAXC3; ++c) t2[c] = (uint32_t)cur.t[c];
-      double acc;
-      switch (C) {
-        case 0: acc = 0.0; break;
-        case 1: acc = dot2<1>(v, t2); break;
-        case 2: acc = dot2<2>(v, t2); break;
-        case 3: acc = dot2<3>(v, t2); break;
-        default: {
-          acc = dot2<4>(v, t2);
-          const int cnt = (int)hc.cnt, li = lane < cnt ? lane : 0;
-          for (int c = MAXC3; c < C; ++c) {
-            const uint32_t t = lane < cnt ? P.terms2[hc.off_terms + c * cnt + li]
-                                          : ((uint32_t)P.ZERO | ((uint32_t)P.ZERO << 16));
-            acc = fma(v[t & 0xffffu], v[t >> 16], acc);
-          }
-        }
-      }
-      acc = group_sum(acc, (int)((hc.cfg >> 8) & 0xffu), (int)((cur.mt >> META_GLOG_SHIFT) & 7u));
-      if (cur.mt & META_HEAD) {
-        const int t = (int)(cur.mt & META_TGT_MASK);
-        v[t] = (cur.mt & META_ZERO) ? -acc : v[t] - acc;
-      }
-    } else {
-      double acc;
-      switch (C) {
-        case 0: acc = 0.0; break;
-        case 1: acc = dot3<1>(v, cur.t); break;
-        case 2: acc = dot3<2>(v, cur.t); break;
-        case 3: acc = dot3<3>(v, cur.t); break;
-        default: {
-          acc = dot3<4>(v, cur.t);
-          const int cnt = (int)hc.cnt, li = lane < cnt ? lane : 0;
-          for (int c = MAXC3; c < C; ++c) {
-            const uint64_t t =
-                lane < cnt ? P.terms3[hc.off_terms + (size_t)c * cnt + li] : dummy3;
-            acc = fma(v[t & 0xffffu] * v[(t >> 16) & 0xffffu], v[t >> 32], acc);
-          }
-        }
-      }
-      acc = group_sum(acc, (int)((hc.cfg >> 8) & 0xffu), (int)((cur.mt >> META_GLOG_SHIFT) & 7u));
-      if (cur.mt & META_HEAD) {
-        const int t = (int)(cur.mt & META_TGT_MASK);
-        const double nv = v[t] - acc;
-        v[t] = nv;
-        if (cur.mt & META_ISD) v[P.DINV + (t - P.W)] = 1.0 / nv;
-      }
-    }
-    LDS_FENCE();
-    cur = nxt;
-    hc = hn;
-  }
+  const uint32_t dshift = (uint32_t)(P.DINV - P.W) * 8u;
+  if (P.nfac > 0) run_fac(P.fac, P.nfac, v, lane, dshift);
+  LDS_FENCE();
+#pragma unroll 4
+  for (int k = lane; k < P.nnzL; k += 64) v[P.LX + k] *= v[P.Lcol[k]];
+  LDS_FENCE();
+  if (P.ntail > 0) run_fac(P.tail, P.ntail, v, lane, dshift);
 }
 
 // constraint classes packed 2 bits per register slot (auxil.c constr_type)
@@ -816,7 +743,6 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
 
 template <int RN, int RM>
 __device__ __forceinline__ void solve_instance(const KParams& p, int inst, double* v, double* scr,
-                                               const uint32_t* tmeta, const uint32_t* tterm,
                                                int lane) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
@@ -915,10 +841,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       if (i < m) v[wsz[r] + coff] = bz[r];
     }
     LDS_FENCE();
-    run_dot2(p, P.fwd, P.nfwd, tmeta, tterm, v, lane);
+    run_solve(P.fwd, P.nfwd, v, lane);
     for (int k = lane; k < P.nk; k += 64) v[P.CACC + k] = v[P.W + k] * v[P.DINV + k];
     LDS_FENCE();
-    run_dot2(p, P.bwd, P.nbwd, tmeta, tterm, v, lane);
+    run_solve(P.bwd, P.nbwd, v, lane);
     // x, z, y updates (auxil.c update_x / update_z / update_y)
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
@@ -1033,42 +959,22 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   }
 }
 
-// One workgroup = WPG <= 8 waves (blockDim.x = 64 * WPG); each wave solves its own instances.  The
-// workgroup's LDS holds one copy of the step headers followed by one instance image per wave.
+// One wave per workgroup; the instance image is the workgroup's whole (dynamic) LDS, at address 0.
 template <int RN, int RM>
-__global__ void __launch_bounds__(512) qp_batch_kernel(KParams p) {
+__global__ void __launch_bounds__(64) qp_batch_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int lane = (int)(threadIdx.x & 63);
-  const int wave = (int)(threadIdx.x >> 6);
-  const int wpg = (int)(blockDim.x >> 6);
-  uint32_t* tbl = reinterpret_cast<uint32_t*>(lds);
-  const uint32_t* hsrc[3] = {reinterpret_cast<const uint32_t*>(p.pl.fwd),
-                             reinterpret_cast<const uint32_t*>(p.pl.bwd),
-                             reinterpret_cast<const uint32_t*>(p.pl.fac)};
-  const int hn[3] = {4 * p.pl.nfwd, 4 * p.pl.nbwd, 4 * p.pl.nfac};
-  int off = 0;
-  for (int q = 0; q < 3; ++q) {
-    for (int k = (int)threadIdx.x; k < hn[q]; k += (int)blockDim.x) tbl[off + k] = hsrc[q][k];
-    off += hn[q];
-  }
-  __syncthreads();
-  KParams q = p;  // schedule headers now read from the workgroup's LDS copy
-  q.pl.fwd = reinterpret_cast<const StepHdr*>(tbl);
-  q.pl.bwd = q.pl.fwd + p.pl.nfwd;
-  q.pl.fac = q.pl.bwd + p.pl.nbwd;
-  // solve-step records stay in global memory (L2-resident, fetched one step ahead)
-  const uint32_t* tmeta = p.pl.smeta;
-  const uint32_t* tterm = p.pl.sterms;
-  double* v = lds + p.pl.tbl_words / 2 + (size_t)wave * p.pl.inst_doubles;
+  const int lane = (int)threadIdx.x;
+  if ((uint32_t)(uintptr_t)lds != 0u) __builtin_trap();  // schedule byte addresses assume base 0
+  double* v = lds;
   const size_t slab = (size_t)(p.pl.nnzP + p.pl.nnzA + 2 * p.pl.n + 2 * p.pl.m);
-  double* scr = p.scratch + ((size_t)blockIdx.x * wpg + wave) * slab;
+  double* scr = p.scratch + (size_t)blockIdx.x * slab;
   for (;;) {
     unsigned int inst = 0;
     if (lane == 0) inst = atomicAdd(p.counter, 1u);
     inst = (unsigned int)__shfl((int)inst, 0);
     inst = __builtin_amdgcn_readfirstlane(inst);
     if (inst >= (unsigned int)p.B) break;
-    solve_instance<RN, RM>(q, (int)inst, v, scr, tmeta, tterm, lane);
+    solve_instance<RN, RM>(p, (int)inst, v, scr, lane);
     LDS_FENCE();
   }
 }
@@ -1134,7 +1040,7 @@ struct mpcqp_handle {
   double* scratch = nullptr;
   unsigned int* counter = nullptr;
   bool has_data = false;
-  int grid = 0, lds_bytes = 0, waves_per_cu = 0, wpg = 1;
+  int grid = 0, lds_bytes = 0, waves_per_cu = 0;
   kernel_fn kern = nullptr;
 };
 
@@ -1198,8 +1104,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   h->set = *s;
   h->B = batch;
   h->stream = (hipStream_t)stream;
-  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, MAXC, MAXC3, h->plan, cap_m(),
-                  cap_w())) {
+  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, h->plan, cap_m(), cap_w())) {
     std::string e = h->plan.error;
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, e);
@@ -1212,19 +1117,17 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   }
   // structure blob
   std::vector<char> blob;
-  size_t o_fac = push_blob(blob, pl.fac), o_fwd = push_blob(blob, pl.fwd),
-         o_bwd = push_blob(blob, pl.bwd), o_meta = push_blob(blob, pl.meta),
-         o_t2 = push_blob(blob, pl.terms2), o_t3 = push_blob(blob, pl.terms3),
-         o_sP = push_blob(blob, pl.slotP), o_sA = push_blob(blob, pl.slotA),
-         o_sR = push_blob(blob, pl.slotRho), o_sS = push_blob(blob, pl.slotSig),
-         o_wx = push_blob(blob, pl.wsx), o_wz = push_blob(blob, pl.wsz),
-         o_Ap = push_blob(blob, pl.Ap), o_Ai = push_blob(blob, pl.Ai),
+  size_t o_fac = push_blob(blob, pl.fac), o_tail = push_blob(blob, pl.tail),
+         o_fwd = push_blob(blob, pl.fwd), o_bwd = push_blob(blob, pl.bwd),
+         o_Lc = push_blob(blob, pl.Lcol), o_sP = push_blob(blob, pl.slotP),
+         o_sA = push_blob(blob, pl.slotA), o_sR = push_blob(blob, pl.slotRho),
+         o_sS = push_blob(blob, pl.slotSig), o_wx = push_blob(blob, pl.wsx),
+         o_wz = push_blob(blob, pl.wsz), o_Ap = push_blob(blob, pl.Ap), o_Ai = push_blob(blob, pl.Ai),
          o_Ac = push_blob(blob, pl.Acol), o_Arp = push_blob(blob, pl.Arp),
          o_Ark = push_blob(blob, pl.Ark), o_Arj = push_blob(blob, pl.Arj),
          o_Pi = push_blob(blob, pl.Pi), o_Pc = push_blob(blob, pl.Pcol),
          o_Psp = push_blob(blob, pl.Psp), o_Psk = push_blob(blob, pl.Psk),
-         o_Pso = push_blob(blob, pl.Pso), o_sm = push_blob(blob, pl.smeta),
-         o_st = push_blob(blob, pl.sterms);
+         o_Pso = push_blob(blob, pl.Pso);
   auto cleanup_fail = [&](int code, const std::string& msg) {
     mpcqp_destroy(h);
     return fail(code, msg);
@@ -1235,11 +1138,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     return cleanup_fail(MPCQP_E_HIP, "hipMemcpy(structure)");
   char* b = h->d_blob;
   DevPlan& dp = h->dp;
-  dp.fac = (const StepHdr*)(b + o_fac), dp.fwd = (const StepHdr*)(b + o_fwd);
-  dp.bwd = (const StepHdr*)(b + o_bwd);
-  dp.nfac = (int)pl.fac.size(), dp.nfwd = (int)pl.fwd.size(), dp.nbwd = (int)pl.bwd.size();
-  dp.meta = (const uint32_t*)(b + o_meta), dp.terms2 = (const uint32_t*)(b + o_t2);
-  dp.terms3 = (const uint64_t*)(b + o_t3);
+  dp.fac = (const uint32_t*)(b + o_fac), dp.tail = (const uint32_t*)(b + o_tail);
+  dp.fwd = (const uint32_t*)(b + o_fwd), dp.bwd = (const uint32_t*)(b + o_bwd);
+  dp.nfac = pl.nfac, dp.ntail = pl.ntail, dp.nfwd = pl.nfwd, dp.nbwd = pl.nbwd;
+  dp.Lcol = (const uint16_t*)(b + o_Lc);
   dp.slotP = (const uint16_t*)(b + o_sP), dp.slotA = (const uint16_t*)(b + o_sA);
   dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
   dp.wsx = (const uint16_t*)(b + o_wx), dp.wsz = (const uint16_t*)(b + o_wz);
@@ -1249,10 +1151,6 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   dp.Pi = (const uint16_t*)(b + o_Pi), dp.Pcol = (const uint16_t*)(b + o_Pc);
   dp.Psp = (const uint16_t*)(b + o_Psp), dp.Psk = (const uint16_t*)(b + o_Psk);
   dp.Pso = (const uint16_t*)(b + o_Pso);
-  dp.smeta = (const uint32_t*)(b + o_sm), dp.sterms = (const uint32_t*)(b + o_st);
-  dp.nsmeta = (int)pl.smeta.size(), dp.nsterms = (int)pl.sterms.size();
-  dp.hdr_words = 4 * (dp.nfwd + dp.nbwd + dp.nfac);
-  dp.tbl_words = (dp.hdr_words + 3) & ~3;
   dp.inst_doubles = (pl.LDS_N + 1) & ~1;
   dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
   dp.nnzL = pl.nnzL;
@@ -1260,32 +1158,25 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N;
   dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
 
-  // occupancy -> workgroup size (waves sharing one LDS copy of the solve tables) and grid
+  // occupancy (LDS image and VGPRs) -> persistent grid
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return cleanup_fail(MPCQP_E_HIP, "hipGetDevice");
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return cleanup_fail(MPCQP_E_HIP, "hipDeviceGetAttribute");
-  const int tbl_bytes = dp.tbl_words * 4, inst_bytes = dp.inst_doubles * 8;
+  const int inst_bytes = dp.inst_doubles * 8;
   const int lds_cap = 160 * 1024;
+  if (inst_bytes > lds_cap)
+    return cleanup_fail(MPCQP_E_UNSUPPORTED, "instance image exceeds the LDS of a CU");
   if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                           lds_cap) != hipSuccess)
     return cleanup_fail(MPCQP_E_HIP, "hipFuncSetAttribute");
-  int best_waves = 0, best_wpg = 0, best_nb = 0;
-  for (int wpg = 1; wpg <= 8; ++wpg) {
-    const int lds = tbl_bytes + wpg * inst_bytes;
-    if (lds > lds_cap) break;
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, 64 * wpg, lds) !=
-        hipSuccess)
-      continue;
-    if (nb * wpg > best_waves) best_waves = nb * wpg, best_wpg = wpg, best_nb = nb;
-  }
-  if (best_waves <= 0)
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, 64, inst_bytes) !=
+          hipSuccess || nb <= 0)
     return cleanup_fail(MPCQP_E_UNSUPPORTED, "kernel does not fit on a CU (LDS/VGPR)");
-  h->wpg = best_wpg;
-  h->waves_per_cu = best_waves;
-  h->lds_bytes = tbl_bytes + best_wpg * inst_bytes;
-  h->grid = std::min((batch + best_wpg - 1) / best_wpg, best_nb * ncu);
+  h->waves_per_cu = nb;
+  h->lds_bytes = inst_bytes;
+  h->grid = std::min(batch, nb * ncu);
   const size_t Bz = (size_t)batch;
   bool ok = hipMalloc(&h->Px, sizeof(double) * std::max(1, pl.nnzP)) == hipSuccess &&
             hipMalloc(&h->q, sizeof(double) * pl.n) == hipSuccess &&
@@ -1298,7 +1189,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->Ecls, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
-            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid * h->wpg *
+            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid *
                                        (pl.nnzP + pl.nnzA + 2 * pl.n + 2 * pl.m)) ==
                 hipSuccess &&
             hipMalloc(&h->counter, 64) == hipSuccess;
@@ -1388,7 +1279,7 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   p.scratch = h->scratch;
   p.counter = h->counter;
   HIPCHK(hipMemsetAsync(h->counter, 0, 64, h->stream));
-  hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(64 * h->wpg), h->lds_bytes, h->stream, p);
+  hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(64), h->lds_bytes, h->stream, p);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1430,9 +1321,9 @@ int mpcqp_dims(const mpcqp_handle* h, int32_t* n, int32_t* m, int32_t* nnzP, int
 int mpcqp_schedule_info(const mpcqp_handle* h, int32_t* fac, int32_t* fwd, int32_t* bwd,
                         int32_t* lds, int32_t* wpc) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");
-  if (fac) *fac = (int32_t)h->plan.fac.size();
-  if (fwd) *fwd = (int32_t)h->plan.fwd.size();
-  if (bwd) *bwd = (int32_t)h->plan.bwd.size();
+  if (fac) *fac = (int32_t)(h->plan.nfac + h->plan.ntail);
+  if (fwd) *fwd = (int32_t)h->plan.nfwd;
+  if (bwd) *bwd = (int32_t)h->plan.nbwd;
   if (lds) *lds = h->lds_bytes;
   if (wpc) *wpc = h->waves_per_cu;
   return 0;
@@ -1442,7 +1333,7 @@ int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t
                   int32_t* nnzL, int32_t* stats) {
   if (!st || !nnzL) return fail(MPCQP_E_INVALID, "null argument");
   Plan pl;
-  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, MAXC, MAXC3, pl, cap_m(), cap_w()))
+  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   const int cap = *nnzL;
   *nnzL = pl.nnzL;
@@ -1450,9 +1341,9 @@ int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t
   if (Lp) std::copy(pl.Lp.begin(), pl.Lp.end(), Lp);
   if (Li && cap >= pl.nnzL) std::copy(pl.Li.begin(), pl.Li.end(), Li);
   if (stats) {
-    stats[0] = (int32_t)pl.fac.size();
-    stats[1] = (int32_t)pl.fwd.size();
-    stats[2] = (int32_t)pl.bwd.size();
+    stats[0] = (int32_t)(pl.nfac + pl.ntail);
+    stats[1] = (int32_t)pl.nfwd;
+    stats[2] = (int32_t)pl.nbwd;
     stats[3] = pl.levels_fwd;
     stats[4] = pl.levels_bwd;
     stats[5] = pl.LDS_N * (int)sizeof(double);

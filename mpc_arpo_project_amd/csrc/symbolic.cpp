@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <array>
 #include <numeric>
 #include <unordered_map>
 
@@ -45,103 +46,107 @@ void min_degree(int nk, std::vector<uint8_t>& adj, std::vector<int32_t>& perm) {
 }
 
 struct Task {
-  uint32_t target;
-  bool isD;
-  std::vector<uint64_t> terms;  // packed a | b << 16 | c << 32
-  bool fromzero = false;
+  int target = 0;        // LDS slot (double index)
+  bool isD = false;      // factorization: also write 1/v[target]
+  bool inplace = false;  // v[t] <- v[t] - sum  (otherwise v[t] <- -sum)
+  std::vector<std::array<int, 3>> terms;  // LDS slots; solve terms use the first two
 };
 
-// Pack one level's tasks into 64-lane steps (see symbolic.hpp).
-void pack_level(std::vector<Task>& tasks, StepKind kind, int max_c, int dummy_slot,
-                std::vector<StepHdr>& steps, std::vector<uint32_t>& meta,
-                std::vector<uint32_t>& terms2, std::vector<uint64_t>& terms3) {
+// Pack one level's tasks into fixed-stride 64-lane steps appended to tbl (see symbolic.hpp).
+// Returns the number of steps.  In-place tasks get the term (-1) * v[t] (times 1 for the
+// factorization); a task with more terms than one step holds is split into chunks that run in
+// consecutive rounds of steps, every chunk after the first in place.
+int pack_level(const std::vector<Task>& tasks, bool fac, const Plan& pl, std::vector<uint32_t>& tbl) {
+  const int maxc = fac ? FAC_MAXC : SOLVE_MAXC;
+  const int cap = 64 * maxc;
+  std::vector<std::vector<Task>> rounds;
+  for (const Task& t : tasks) {
+    size_t pos = 0;
+    for (int r = 0; r == 0 || pos < t.terms.size(); ++r) {
+      Task c;
+      c.target = t.target;
+      c.isD = t.isD;
+      const bool self = t.inplace || r > 0;
+      if (self) c.terms.push_back({pl.MONE, t.target, pl.ONE});
+      const size_t take = std::min(t.terms.size() - pos, (size_t)(cap - (self ? 1 : 0)));
+      c.terms.insert(c.terms.end(), t.terms.begin() + pos, t.terms.begin() + pos + take);
+      pos += take;
+      if ((int)rounds.size() <= r) rounds.resize(r + 1);
+      rounds[r].push_back(std::move(c));
+    }
+  }
   struct Placed {
     const Task* t;
     int g, glog, c;
   };
-  std::vector<Placed> pl;
-  for (auto& t : tasks) {
-    int nt = (int)t.terms.size();
-    int g = 1, glog = 0;
-    while (g < 64 && (nt + g - 1) / g > max_c) g *= 2, glog++;
-    int c = (nt + g - 1) / g;
-    pl.push_back({&t, g, glog, c});
-  }
-  // widest groups first keeps groups aligned; then by C so that similar tasks share a step
-  std::stable_sort(pl.begin(), pl.end(), [](const Placed& a, const Placed& b) {
-    if (a.g != b.g) return a.g > b.g;
-    return a.c > b.c;
-  });
-  const uint64_t dummy = (uint64_t)dummy_slot | ((uint64_t)dummy_slot << 16) |
-                         ((uint64_t)dummy_slot << 32);
-  size_t i = 0;
-  while (i < pl.size()) {
-    // gather tasks for one step
-    std::vector<std::pair<int, const Placed*>> in;  // lane offset, task
-    int cur = 0, C = 0, glog = 0;
-    while (i < pl.size()) {
-      int off = (cur + pl[i].g - 1) / pl[i].g * pl[i].g;
-      if (off + pl[i].g > 64) break;
-      in.push_back({off, &pl[i]});
-      cur = off + pl[i].g;
-      C = std::max(C, pl[i].c);
-      glog = std::max(glog, pl[i].glog);
-      i++;
+  const uint32_t zb = (uint32_t)pl.ZERO * 8u;
+  int nsteps = 0;
+  for (const auto& rt : rounds) {
+    std::vector<Placed> pv;
+    for (const Task& t : rt) {
+      const int nt = (int)t.terms.size();
+      int g = 1, glog = 0;
+      while (g < 64 && (nt + g - 1) / g > maxc) g *= 2, glog++;
+      pv.push_back({&t, g, glog, (nt + g - 1) / g});
     }
-    int cnt = cur;
-    StepHdr h;
-    h.off_meta = (uint32_t)meta.size();
-    h.off_terms = kind == KIND_DOT3 ? (uint32_t)terms3.size() : (uint32_t)terms2.size();
-    h.cnt = (uint32_t)cnt;
-    h.cfg = (uint32_t)C | ((uint32_t)glog << 8) | ((uint32_t)kind << 16);
-    std::vector<uint32_t> mrow(cnt, 0);
-    std::vector<uint64_t> trow((size_t)C * cnt, dummy);
-    for (auto& pr : in) {
-      int off = pr.first;
-      const Placed* p = pr.second;
-      for (int r = 0; r < p->g; r++) {
-        uint32_t mt = META_ACTIVE | ((uint32_t)p->glog << META_GLOG_SHIFT);
-        mt |= p->t->target & META_TGT_MASK;
-        if (r == 0) mt |= META_HEAD;
-        if (p->t->isD) mt |= META_ISD;
-        if (p->t->fromzero) mt |= META_ZERO;
-        mrow[off + r] = mt;
+    // widest groups first keeps groups aligned; then by C so that similar tasks share a step
+    std::stable_sort(pv.begin(), pv.end(), [](const Placed& x, const Placed& y) {
+      if (x.g != y.g) return x.g > y.g;
+      return x.c > y.c;
+    });
+    size_t i = 0;
+    while (i < pv.size()) {
+      std::vector<std::pair<int, const Placed*>> in;  // lane offset, task
+      int cur = 0, C = 0, glog = 0;
+      while (i < pv.size()) {
+        const int off = (cur + pv[i].g - 1) / pv[i].g * pv[i].g;
+        if (off + pv[i].g > 64) break;
+        in.push_back({off, &pv[i]});
+        cur = off + pv[i].g;
+        C = std::max(C, pv[i].c);
+        glog = std::max(glog, pv[i].glog);
+        i++;
       }
-      const auto& tv = p->t->terms;
-      for (size_t q = 0; q < tv.size(); q++) {
-        int lane = off + (int)(q % p->g);
-        int c = (int)(q / p->g);
-        trow[(size_t)c * cnt + lane] = tv[q];
+      const size_t base = tbl.size();
+      tbl.resize(base + STEP_WORDS, zb);
+      uint32_t* st = tbl.data() + base;
+      // idle lanes of a solve step store to their own sink slot (the device stores
+      // unconditionally); group lanes other than the head store the same value as the head
+      for (int l = 0; l < 64; ++l)
+        st[l] = ((uint32_t)C << META_C_SHIFT) | ((uint32_t)glog << META_SGLOG_SHIFT) |
+                (fac ? 0u : (uint32_t)(pl.SINK + l) * 8u);
+      for (auto& pr : in) {
+        const int off = pr.first;
+        const Placed* p = pr.second;
+        for (int r = 0; r < p->g; r++) {
+          uint32_t mt = ((uint32_t)p->glog << META_GLOG_SHIFT) | ((uint32_t)p->t->target * 8u);
+          if (r == 0) mt |= META_HEAD;
+          if (p->t->isD) mt |= META_ISD;
+          st[off + r] = (st[off + r] & ~META_TGT_MASK) | mt;
+        }
+        const auto& tv = p->t->terms;
+        for (size_t q = 0; q < tv.size(); q++) {
+          const int lane = off + (int)(q % p->g), c = (int)(q / p->g);
+          if (fac) {
+            uint32_t* w = st + 64 + c * 256 + lane * 4;
+            w[0] = (uint32_t)tv[q][0] * 8u, w[1] = (uint32_t)tv[q][1] * 8u;
+            w[2] = (uint32_t)tv[q][2] * 8u;
+          } else {
+            uint32_t* w = st + 64 + c * 128 + lane * 2;
+            w[0] = (uint32_t)tv[q][0] * 8u, w[1] = (uint32_t)tv[q][1] * 8u;
+          }
+        }
       }
+      nsteps++;
     }
-    meta.insert(meta.end(), mrow.begin(), mrow.end());
-    if (kind == KIND_DOT3) {
-      terms3.insert(terms3.end(), trow.begin(), trow.end());
-    } else {
-      for (auto t : trow) terms2.push_back((uint32_t)(t & 0xffffffffu));
-    }
-    steps.push_back(h);
   }
-}
-
-void pack_scale(const std::vector<uint32_t>& entries, std::vector<StepHdr>& steps,
-                std::vector<uint32_t>& terms2) {
-  for (size_t s = 0; s < entries.size(); s += 64) {
-    size_t cnt = std::min<size_t>(64, entries.size() - s);
-    StepHdr h;
-    h.off_meta = 0;
-    h.off_terms = (uint32_t)terms2.size();
-    h.cnt = (uint32_t)cnt;
-    h.cfg = 1u | ((uint32_t)KIND_SCALE << 16);
-    terms2.insert(terms2.end(), entries.begin() + s, entries.begin() + s + cnt);
-    steps.push_back(h);
-  }
+  return nsteps;
 }
 
 }  // namespace
 
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, int max_c, int max_c3, Plan& pl, int capM, int capW) {
+                const int32_t* Ai, Plan& pl, int capM, int capW) {
   pl = Plan();
   pl.n = n, pl.m = m, pl.nk = n + m;
   const int nk = n + m;
@@ -337,7 +342,8 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   pl.ZERO = pl.GPB + pl.nGP;
   pl.ONE = pl.ZERO + 1;
   pl.MONE = pl.ZERO + 2;
-  pl.LDS_N = pl.ZERO + 4;  // keeps the image a multiple of 16 bytes with an even base
+  pl.SINK = pl.ZERO + 4;    // 64 sink slots for idle lanes of solve steps
+  pl.LDS_N = pl.SINK + 64;  // keeps the image a multiple of 16 bytes with an even base
   // slot of N_{r r2} (r2 in reach(r) or r2 == r -> MONE), G_{r x}, G'_{r z}
   auto nslot = [&](int r, int r2) -> int {
     if (r2 == r) return pl.MONE;
@@ -361,8 +367,8 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   if (pl.S_ET + m > pl.LDS_N) pl.LDS_N = pl.S_ET + m;
   pl.LDS_N = (pl.LDS_N + 1) & ~1;
   // the residual SpMVs stage x (n) and y (m) as plain arrays in the W + C regions
-  if (pl.LDS_N >= 65535) {
-    pl.error = "LDS image too large for 16-bit slots";
+  if (pl.LDS_N * 8 > (int)META_TGT_MASK || pl.LDS_N >= 65535) {
+    pl.error = "LDS image too large for the schedule's byte addresses";
     return false;
   }
 
@@ -414,54 +420,51 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   std::vector<std::vector<int>> bylev(maxlev + 1), byblev(maxblev + 1);
   for (int i = 0; i < nk; i++) bylev[lev[i]].push_back(i), byblev[blev[i]].push_back(i);
 
-  const int Z = pl.ZERO;
-  auto T2 = [](int a, int b) { return (uint64_t)a | ((uint64_t)b << 16); };
-  auto T3 = [](int a, int b, int c) {
-    return (uint64_t)a | ((uint64_t)b << 16) | ((uint64_t)c << 32);
-  };
-
-  // ---- factorization schedule: per level, dot tasks (D_j and numerators of L_ij) then scaling
+  // ---- factorization of U = L D (U_ij = L_ij D_j) and D, by levels of the elimination tree:
+  //   D_j  = K_jj - sum_{k in lrow(j)} U_jk U_jk / D_k
+  //   U_ij = K_ij - sum_{k in lrow(j) ^ lrow(i)} U_ik U_jk / D_k
   for (int L = 0; L <= maxlev; L++) {
     std::vector<Task> tasks;
-    std::vector<uint32_t> scal;
     for (int j : bylev[L]) {
       Task d;
-      d.target = (uint32_t)(pl.W + j);
+      d.target = pl.W + j;
       d.isD = true;
+      d.inplace = true;
       for (int k : lrow[j]) {
-        int pjk = lpos(j, k);
-        d.terms.push_back(T3(pl.LX + pjk, pl.LX + pjk, pl.W + k));
+        const int pjk = lpos(j, k);
+        d.terms.push_back({pl.LX + pjk, pl.LX + pjk, pl.DINV + k});
       }
       tasks.push_back(std::move(d));
       for (int i : lcol[j]) {
         Task t;
-        t.target = (uint32_t)(pl.LX + lpos(i, j));
-        t.isD = false;
-        // k in lrow[j] ∩ lrow[i]
-        const auto& a = lrow[j];
+        t.target = pl.LX + lpos(i, j);
+        t.inplace = true;
+        const auto& a = lrow[j];  // k in lrow[j] ^ lrow[i]
         const auto& b = lrow[i];
         size_t x = 0, y = 0;
         while (x < a.size() && y < b.size()) {
-          if (a[x] < b[y])
+          if (a[x] < b[y]) {
             x++;
-          else if (a[x] > b[y])
+          } else if (a[x] > b[y]) {
             y++;
-          else {
-            int k = a[x];
-            t.terms.push_back(T3(pl.LX + lpos(i, k), pl.LX + lpos(j, k), pl.W + k));
+          } else {
+            const int k = a[x];
+            t.terms.push_back({pl.LX + lpos(i, k), pl.LX + lpos(j, k), pl.DINV + k});
             x++, y++;
           }
         }
         if (!t.terms.empty()) tasks.push_back(std::move(t));
-        scal.push_back((uint32_t)(pl.LX + lpos(i, j)) | ((uint32_t)(pl.DINV + j) << 16));
       }
     }
-    pack_level(tasks, KIND_DOT3, max_c3, Z, pl.fac, pl.meta, pl.terms2, pl.terms3);
-    pack_scale(scal, pl.fac, pl.terms2);
+    pl.nfac += pack_level(tasks, true, pl, pl.fac);
   }
-  // ---- factorization tail: N (negated block inverses), then G and G' (one level)
+  pl.Lcol.resize(pl.nnzL);
+  for (int j = 0; j < nk; j++)
+    for (int p = pl.Lp[j]; p < pl.Lp[j + 1]; p++) pl.Lcol[p] = (uint16_t)(pl.DINV + j);
+  // ---- factorization tail (after L = U / D): N (negated block inverses) by depth in the block,
+  // then G and G' (one level).  Two-factor terms carry the ONE slot as third factor.
   {
-    // N_{r r2} = -sum_{t in lrow(r), r2 <= t < r} L_{rt} N_{t r2}   (N_{tt} = -1), by depth in block
+    // N_{r r2} = -sum_{t in lrow(r), r2 <= t < r} L_{rt} N_{t r2}   (N_{tt} = -1)
     std::vector<int> depth(nk, 0);
     int maxd = 0;
     for (int r = 0; r < nk; r++) {
@@ -475,52 +478,46 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
         if (depth[r] != dl) continue;
         for (int r2 : reach[r]) {
           Task t;
-          t.target = (uint32_t)nslot(r, r2);
-          t.isD = false;
-          t.fromzero = true;
+          t.target = nslot(r, r2);
           for (int tt : lrow[r]) {
             if (tt < r2) continue;
-            int ns = nslot(tt, r2);
+            const int ns = nslot(tt, r2);
             if (ns < 0) continue;
-            t.terms.push_back(T2(pl.LX + lpos(r, tt), ns));
+            t.terms.push_back({pl.LX + lpos(r, tt), ns, pl.ONE});
           }
           tasks.push_back(std::move(t));
         }
       }
-      pack_level(tasks, KIND_DOT2, max_c3, Z, pl.fac, pl.meta, pl.terms2, pl.terms3);
+      pl.ntail += pack_level(tasks, true, pl, pl.tail);
     }
     std::vector<Task> tasks;
     for (int r = 0; r < nk; r++) {
       // G_{r x} = -sum_{r2 in reach(r) U {r}} N_{r r2} L_{r2 x}
       for (int x : gpat[r]) {
         Task t;
-        t.target = (uint32_t)gslot(r, x);
-        t.isD = false;
-        t.fromzero = true;
+        t.target = gslot(r, x);
         std::vector<int> src(reach[r].begin(), reach[r].end());
         src.push_back(r);
         for (int r2 : src) {
-          int p = lpos(r2, x);
-          if (p >= 0) t.terms.push_back(T2(nslot(r, r2), pl.LX + p));
+          const int p = lpos(r2, x);
+          if (p >= 0) t.terms.push_back({nslot(r, r2), pl.LX + p, pl.ONE});
         }
         tasks.push_back(std::move(t));
       }
       // G'_{r z} = -sum_{r2: r in reach(r2) or r2 == r} N_{r2 r} L_{z r2}
       for (int z : gppat[r]) {
         Task t;
-        t.target = (uint32_t)gpslot(r, z);
-        t.isD = false;
-        t.fromzero = true;
+        t.target = gpslot(r, z);
         std::vector<int> src(rtr[r].begin(), rtr[r].end());
         src.push_back(r);
         for (int r2 : src) {
-          int p = lpos(z, r2);
-          if (p >= 0) t.terms.push_back(T2(nslot(r2, r), pl.LX + p));
+          const int p = lpos(z, r2);
+          if (p >= 0) t.terms.push_back({nslot(r2, r), pl.LX + p, pl.ONE});
         }
         tasks.push_back(std::move(t));
       }
     }
-    pack_level(tasks, KIND_DOT2, max_c3, Z, pl.fac, pl.meta, pl.terms2, pl.terms3);
+    pl.ntail += pack_level(tasks, true, pl, pl.tail);
   }
   // ---- forward solve (input C = rhs, output W): per block k
   //   W_r = sum_{r2 in reach(r) U {r}} M_{r r2} C_{r2} - sum_{x in block k-1} G_{r x} W_x
@@ -529,24 +526,22 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     std::vector<Task> tasks;
     for (int r = bs(k); r < be(k); r++) {
       Task t;
-      t.target = (uint32_t)(pl.W + r);
-      t.isD = false;
-      t.fromzero = true;
-      for (int r2 : reach[r]) t.terms.push_back(T2(nslot(r, r2), pl.CACC + r2));
-      t.terms.push_back(T2(pl.MONE, pl.CACC + r));
-      for (int x : gpat[r]) t.terms.push_back(T2(gslot(r, x), pl.W + x));
+      t.target = pl.W + r;
+      for (int r2 : reach[r]) t.terms.push_back({nslot(r, r2), pl.CACC + r2, 0});
+      t.terms.push_back({pl.MONE, pl.CACC + r, 0});
+      for (int x : gpat[r]) t.terms.push_back({gslot(r, x), pl.W + x, 0});
       tasks.push_back(std::move(t));
     }
     if (k >= 1)
       for (int r = be(k); r < nk; r++) {
         Task t;
-        t.target = (uint32_t)(pl.CACC + r);
-        t.isD = false;
+        t.target = pl.CACC + r;
+        t.inplace = true;
         for (int x : lrow[r])
-          if (x >= bs(k - 1) && x < be(k - 1)) t.terms.push_back(T2(pl.LX + lpos(r, x), pl.W + x));
+          if (x >= bs(k - 1) && x < be(k - 1)) t.terms.push_back({pl.LX + lpos(r, x), pl.W + x, 0});
         if (!t.terms.empty()) tasks.push_back(std::move(t));
       }
-    pack_level(tasks, KIND_DOT2, max_c, Z, pl.fwd, pl.smeta, pl.sterms, pl.terms3);
+    pl.nfwd += pack_level(tasks, false, pl, pl.fwd);
   }
   // ---- backward solve (input C = D^-1 W, output W): blocks in reverse
   //   W_r = sum_{r2: r in reach(r2) or r2 == r} M_{r2 r} C_{r2} - sum_{z in block k+1} G'_{r z} W_z
@@ -555,24 +550,22 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     std::vector<Task> tasks;
     for (int r = bs(k); r < be(k); r++) {
       Task t;
-      t.target = (uint32_t)(pl.W + r);
-      t.isD = false;
-      t.fromzero = true;
-      for (int r2 : rtr[r]) t.terms.push_back(T2(nslot(r2, r), pl.CACC + r2));
-      t.terms.push_back(T2(pl.MONE, pl.CACC + r));
-      for (int z : gppat[r]) t.terms.push_back(T2(gpslot(r, z), pl.W + z));
+      t.target = pl.W + r;
+      for (int r2 : rtr[r]) t.terms.push_back({nslot(r2, r), pl.CACC + r2, 0});
+      t.terms.push_back({pl.MONE, pl.CACC + r, 0});
+      for (int z : gppat[r]) t.terms.push_back({gpslot(r, z), pl.W + z, 0});
       tasks.push_back(std::move(t));
     }
     if (k + 1 < T)
       for (int r = 0; r < bs(k); r++) {
         Task t;
-        t.target = (uint32_t)(pl.CACC + r);
-        t.isD = false;
+        t.target = pl.CACC + r;
+        t.inplace = true;
         for (int z : lcol[r])
-          if (z >= bs(k + 1) && z < be(k + 1)) t.terms.push_back(T2(pl.LX + lpos(z, r), pl.W + z));
+          if (z >= bs(k + 1) && z < be(k + 1)) t.terms.push_back({pl.LX + lpos(z, r), pl.W + z, 0});
         if (!t.terms.empty()) tasks.push_back(std::move(t));
       }
-    pack_level(tasks, KIND_DOT2, max_c, Z, pl.bwd, pl.smeta, pl.sterms, pl.terms3);
+    pl.nbwd += pack_level(tasks, false, pl, pl.bwd);
   }
   pl.levels_fwd = T;
   pl.levels_bwd = T;

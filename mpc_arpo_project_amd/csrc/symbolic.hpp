@@ -7,13 +7,18 @@
 // a batch share the pattern, everything here is computed once per handle; per-instance work on
 // the GPU is purely numeric.
 //
-// Level schedules.  Factorization (left-looking, dot-product form), forward solve L w = b and
-// backward solve L' x = w are each cut into levels of mutually independent "tasks"; a task writes
-// one LDS slot  v[t] <- v[t] - sum_k prod(terms_k)  (2-factor terms for the solves, 3-factor terms
-// L_ik * L_jk * D_k for the factorization).  A level is packed into one or more 64-lane "steps":
-// a task gets an aligned group of g = 2^glog lanes, each lane accumulates <= C terms and the group
-// reduces with an xor butterfly; the group's first lane writes the slot.  Scale steps apply
-// L_ij *= 1/D_j after each factorization level.
+// Level schedules.  Factorization (left-looking, dot-product form on U = L D), forward solve
+// L w = b and backward solve L' x = w are each cut into levels of mutually independent "tasks"; a
+// task SETS one LDS slot  v[t] <- -sum_k prod(terms_k)  (2-factor terms for the solves, 3-factor
+// terms U_ik * U_jk * (1/D_k) for the factorization).  A task that updates its slot in place gets
+// the extra term (-1) * v[t], so the device never reads its target back.  A level is packed into
+// 64-lane "steps": a task gets an aligned group of g = 2^glog lanes, each lane accumulates <= C
+// terms and the group reduces with an xor butterfly; the group's first lane writes the slot.
+//
+// Step records have a fixed stride (STEP_WORDS 32-bit words) so that the device computes no
+// record addresses: word [lane] is the lane's meta word, then MAXC rows of 64 lane records of
+// absolute LDS byte addresses: (a, b) pairs for the solves, (a, b, c, 0) quads for the
+// factorization.  Unused lanes / terms point at the image's ZERO slot.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -21,30 +26,26 @@
 
 namespace mpcqp {
 
-enum StepKind : uint32_t { KIND_DOT2 = 0, KIND_DOT3 = 1, KIND_SCALE = 2 };
+constexpr int SOLVE_MAXC = 8;   // terms per lane of a solve step
+constexpr int FAC_MAXC = 4;     // terms per lane of a factorization step
+constexpr int STEP_WORDS = 64 + 64 * 2 * SOLVE_MAXC;
+static_assert(STEP_WORDS == 64 + 64 * 4 * FAC_MAXC, "solve and factor steps share a stride");
 
-// One 64-lane step.  meta[off_meta + lane], terms[off_terms + c * cnt + lane] for lane < cnt.
-struct StepHdr {
-  uint32_t off_meta;
-  uint32_t off_terms;
-  uint32_t cnt;  // lanes with a record (<= 64)
-  uint32_t cfg;  // C | glog << 8 | kind << 16
-};
-
-// meta bits
-constexpr uint32_t META_TGT_MASK = 0xffffu;
-constexpr int META_GLOG_SHIFT = 16;  // 3 bits: this lane's group size log2
-constexpr uint32_t META_HEAD = 1u << 19;
-constexpr uint32_t META_ISD = 1u << 20;  // factorization: target is D_j -> also write 1/D_j
-constexpr uint32_t META_ZERO = 1u << 21; // v[t] <- -sum (instead of v[t] - sum)
-constexpr uint32_t META_ACTIVE = 1u << 31;
+// meta word: per-lane fields, then the step-wide C and glog (identical in every lane)
+constexpr uint32_t META_TGT_MASK = 0x1ffffu;  // LDS byte address of the target
+constexpr int META_GLOG_SHIFT = 17;           // 3 bits: this lane's group size log2
+constexpr uint32_t META_HEAD = 1u << 20;
+constexpr uint32_t META_ISD = 1u << 21;       // factorization: target is D_j -> also write 1/D_j
+constexpr int META_C_SHIFT = 22;              // 4 bits: terms per lane in this step
+constexpr int META_SGLOG_SHIFT = 26;          // 3 bits: widest group log2 in this step
 
 struct Plan {
   int n = 0, m = 0, nk = 0, nnzP = 0, nnzA = 0, nnzL = 0;
   std::vector<int32_t> perm, pinv, Lp, Li, etree;
   // LDS layout, in doubles: L | 1/D | W (solve vector) | C (accumulators) | N (negated block
-  // inverses) | G | G' | ZERO ONE MONE pad
+  // inverses) | G | G' | ZERO ONE MONE pad | SINK (64 slots)
   int LX = 0, DINV = 0, W = 0, CACC = 0, NB = 0, GB = 0, GPB = 0, ZERO = 0, ONE = 0, MONE = 0;
+  int SINK = 0;
   int LDS_N = 0;
   // blocked substitution: contiguous blocks of the permuted order
   std::vector<int32_t> block_start;  // T + 1 entries
@@ -56,11 +57,11 @@ struct Plan {
   std::vector<uint16_t> slotP, slotA, slotRho, slotSig;
   // LDS slot (permuted position in the W region) of x_i and z_i
   std::vector<uint16_t> wsx, wsz;
-  // schedules
-  std::vector<StepHdr> fac, fwd, bwd;
-  std::vector<uint32_t> meta, terms2;    // factorization pools (global memory)
-  std::vector<uint32_t> smeta, sterms;   // solve pools (copied into LDS, shared per workgroup)
-  std::vector<uint64_t> terms3;
+  // schedules (STEP_WORDS words per step): factorization of U = L D and D by levels, then
+  // (after the flat pass L = U * (1/D)_col) the block-inverse tail; forward and backward solves
+  std::vector<uint32_t> fac, tail, fwd, bwd;
+  int nfac = 0, ntail = 0, nfwd = 0, nbwd = 0;
+  std::vector<uint16_t> Lcol;  // column of each L entry (the flat scaling pass)
   // matrix structure for scaling / residual SpMVs
   std::vector<uint16_t> Ap, Ai, Acol;  // CSC of A (Ap has n+1 entries, fits: nnzA < 65536)
   std::vector<uint16_t> Arp, Ark;      // CSR of A: row pointers, CSC position of each entry
@@ -73,11 +74,8 @@ struct Plan {
 };
 
 // Builds the plan; returns false (with plan.error set) if the structure is unsupported.
-// max_c / max_c3: max terms per lane per solve / factorization step before a task is widened to
-// more lanes.
 // capM / capW: per block, max entries of the block inverse and max solve terms of its w-tasks.
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, int max_c, int max_c3, Plan& plan, int capM = 128,
-                int capW = 384);
+                const int32_t* Ai, Plan& plan, int capM = 128, int capW = 384);
 
 }  // namespace mpcqp

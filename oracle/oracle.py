@@ -254,16 +254,22 @@ def batch_solve(P, q, A_pattern, Ax_batch, l_batch, u_batch, nthreads=1, **setti
 
 
 def batch_update_solve(solvers, Ax_batch, l_batch, u_batch, nthreads=1):
-    """Warm per-step update + solve of a list of OracleOSQP objects in C threads."""
+    """Warm per-step update + solve of a list of OracleOSQP objects in C threads (None skips the
+    corresponding update; all None: solve the current data)."""
     B = len(solvers)
     n = solvers[0].n
     arr = (C.c_void_p * B)(*[s._w for s in solvers])
-    Ax_batch = np.ascontiguousarray(Ax_batch, dtype=np.float64)
-    l_batch = np.ascontiguousarray(np.maximum(l_batch, -OSQP_INFTY), dtype=np.float64)
-    u_batch = np.ascontiguousarray(np.minimum(u_batch, OSQP_INFTY), dtype=np.float64)
+    null = C.POINTER(C.c_double)()
+    pAx = pl = pu = null
+    if Ax_batch is not None:
+        Ax_batch = np.ascontiguousarray(Ax_batch, dtype=np.float64)
+        pAx = _dp(Ax_batch)
+    if l_batch is not None:
+        l_batch = np.ascontiguousarray(np.maximum(l_batch, -OSQP_INFTY), dtype=np.float64)
+        u_batch = np.ascontiguousarray(np.minimum(u_batch, OSQP_INFTY), dtype=np.float64)
+        pl, pu = _dp(l_batch), _dp(u_batch)
     x = np.empty((B, n))
     st = np.empty(B, dtype=np.int32)
     it = np.empty(B, dtype=np.int32)
-    lib().oqp_batch_update_solve(B, arr, _dp(Ax_batch), _dp(l_batch), _dp(u_batch), nthreads,
-                                 _dp(x), _ip(st), _ip(it))
+    lib().oqp_batch_update_solve(B, arr, pAx, pl, pu, nthreads, _dp(x), _ip(st), _ip(it))
     return x, st, it

@@ -1288,8 +1288,8 @@ static void *warm_worker(void *arg) {
   for (int b = j->b0; b < j->b1; b++) {
     oqp_work *w = j->works[b];
     int nnzA = csc_nnz(w->A);
-    oqp_update_bounds(w, j->l + (size_t)b * w->m, j->u + (size_t)b * w->m);
-    oqp_update_A(w, j->Ax + (size_t)b * nnzA);
+    if (j->l && j->u) oqp_update_bounds(w, j->l + (size_t)b * w->m, j->u + (size_t)b * w->m);
+    if (j->Ax) oqp_update_A(w, j->Ax + (size_t)b * nnzA);
     oqp_solve(w);
     if (j->x) oqp_get_x(w, j->x + (size_t)b * w->n);
     if (j->status) j->status[b] = w->status;

@@ -93,7 +93,8 @@ int oqp_batch_solve(int B, int n, int m, const int *Pp, const int *Pi, const dou
 
 /* Warm closed-loop step for B persistent solvers (the reference's per-step hot path:
  * update(l, u) + update(Ax) + solve, src/trajectorySimulate.py:296,342,348), spread over
- * `nthreads` threads.  Outputs x [B*n], status, iter (any may be NULL). */
+ * `nthreads` threads.  Outputs x [B*n], status, iter (any may be NULL).  With l/u (or Ax) NULL
+ * the corresponding update is skipped (Ax = l = u = NULL: plain solve of the current data). */
 int oqp_batch_update_solve(int B, oqp_work **works, const double *Ax_batch, const double *l_batch,
                            const double *u_batch, int nthreads, double *x_out, int *status_out,
                            int *iter_out);

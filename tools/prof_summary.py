@@ -1,0 +1,46 @@
+"""Summarise a rocprofv3 kernel trace of bench.py: the solve kernel's per-launch duration over the
+TIMED launches only (the first `--warmup` launches are bench.py's untimed warm-up steps), so it can
+be compared with the HIP-event `kernel_ms_per_launch` that bench.py reports.
+
+    python tools/prof_summary.py <run_kernel_trace.csv> <bench.json> [--warmup 3] > summary.json
+"""
+import argparse
+import csv
+import json
+
+import numpy as np
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("bench")
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--kernel", default="qp_batch_kernel")
+    a = ap.parse_args()
+    bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
+    warm = bench["warmup"] if a.warmup is None else a.warmup
+    rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    dur = np.array([int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]) * 1e-6
+    timed = dur[warm:]
+    r0 = rows[0]
+    out = {
+        "kernel": r0["Kernel_Name"],
+        "launches_total": len(rows),
+        "launches_timed": int(timed.size),
+        "rocprof_ms_per_launch_timed": float(timed.mean()),
+        "rocprof_ms_min": float(timed.min()),
+        "rocprof_ms_max": float(timed.max()),
+        "bench_hip_event_ms_per_launch": bench["roofline"]["kernel_ms_per_launch"],
+        "agreement": float(timed.mean() / bench["roofline"]["kernel_ms_per_launch"]),
+        "vgpr": int(r0["VGPR_Count"]), "agpr": int(r0["Accum_VGPR_Count"]),
+        "sgpr": int(r0["SGPR_Count"]), "lds_bytes": int(r0["LDS_Block_Size"]),
+        "scratch": int(r0["Scratch_Size"]), "workgroup": int(r0["Workgroup_Size_X"]),
+        "grid": int(r0["Grid_Size_X"]),
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
