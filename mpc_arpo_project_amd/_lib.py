@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpcqp.so")
+# MPCQP_LIBRARY selects another build of the same ABI (diagnostic builds in tools/); there is no
+# fallback to anything else
+LIB_PATH = os.environ.get("MPCQP_LIBRARY") or os.path.join(_HERE, "libmpcqp.so")
 
 # every symbol include/mpcqp.h declares (checked by tests/test_abi.py)
 EXPORTED = (

@@ -65,7 +65,21 @@ struct KParams {
   mpcqp_info info;
   double* scratch;  // [grid][nnzP + nnzA] scaled P and A values of the wave's current instance
   unsigned int* counter;
+  unsigned long long* timing;  // diagnostic builds only (MPCQP_TIMING): cycles per phase
 };
+
+// Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
+// s_memtime deltas accumulated per wave in SGPRs, added to p.timing at the end of each instance.
+enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_NSLOT };
+#ifdef MPCQP_TIMING
+#define T_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define T_END(slot, v) tacc[slot] += __builtin_amdgcn_s_memtime() - (v)
+#define T_COUNT(slot) tacc[slot] += 1
+#else
+#define T_BEGIN(v)
+#define T_END(slot, v)
+#define T_COUNT(slot)
+#endif
 
 // Ordering between dependent wave-synchronous LDS phases.  A wave's LDS instructions are executed
 // in issue order, so a ds_read issued after a ds_write observes it; only the compiler has to be
@@ -111,17 +125,18 @@ __device__ __forceinline__ double dpp_d(double x) {
   return __hiloint2double(hi, lo);
 }
 // all-reduce of acc over this lane's aligned group of 2^gl lanes (glog = widest group of the step,
-// wave-uniform)
+// wave-uniform); stages beyond the step's widest group are skipped by uniform branches
 __device__ __forceinline__ double group_sum(double acc, uint32_t glog, uint32_t gl) {
   if (glog > 0) {
+    const bool g0 = gl > 0, g1 = gl > 1, g2 = gl > 2;
     const double o = dpp_d<0xB1>(acc);  // quad_perm [1,0,3,2]
-    if (gl > 0) acc += o;
+    acc = g0 ? acc + o : acc;
     if (glog > 1) {
       const double o2 = dpp_d<0x4E>(acc);  // quad_perm [2,3,0,1]
-      if (gl > 1) acc += o2;
+      acc = g1 ? acc + o2 : acc;
       if (glog > 2) {
         const double o3 = dpp_d<0x141>(acc);  // row_half_mirror
-        if (gl > 2) acc += o3;
+        acc = g2 ? acc + o3 : acc;
         if (glog > 3) {
           const double o4 = dpp_d<0x140>(acc);  // row_mirror
           if (gl > 3) acc += o4;
@@ -136,60 +151,58 @@ __device__ __forceinline__ double group_sum(double acc, uint32_t glog, uint32_t 
   return acc;
 }
 
-// one lane's records of a solve step: meta word + SOLVE_MAXC (a, b) address pairs
+// Schedule records are read through buffer descriptors: table base and size in SGPRs, the step
+// offset in an SGPR (soffset), the lane's offset a constant VGPR, so no record address is computed
+// per step.  Reads past the table return 0 (buffer range checking).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc table_rsrc(const uint32_t* tbl, int nsteps, int stride_words) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(tbl), (short)0,
+                                           nsteps * stride_words * 4, 0x00020000);
+}
+
+// one lane's records of a solve step: 4 segment quads (a0, b0, a1, b1), targets t0..t3, meta
 struct SolveRec {
+  uint32_t a[SOLVE_MAXC], b[SOLVE_MAXC];
+  uint32_t t0, t1, t2, t3;
   uint32_t mt;
-  uint2 t[SOLVE_MAXC];
 };
-__device__ __forceinline__ void load_solve(const uint32_t* step, int lane, SolveRec& r) {
-  r.mt = step[lane];
-  const uint2* tp = reinterpret_cast<const uint2*>(step + 64) + lane;
+__device__ __forceinline__ void load_solve(Rsrc rs, int soff, uint32_t lane, SolveRec& r) {
 #pragma unroll
-  for (int c = 0; c < SOLVE_MAXC; ++c) r.t[c] = tp[c * 64];
+  for (int q = 0; q < SOLVE_MAXC / 2; ++q) {
+    const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + q * 1024, soff, 0);
+    r.a[2 * q] = w[0], r.b[2 * q] = w[1], r.a[2 * q + 1] = w[2], r.b[2 * q + 1] = w[3];
+  }
+  const auto tg =
+      __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + 4 * SOLVE_TERM_WORDS, soff, 0);
+  r.t0 = tg[0], r.t1 = tg[1], r.t2 = tg[2], r.t3 = tg[3];
+  r.mt = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lane * 4u) + 4 * SOLVE_TERM_WORDS + 1024,
+                                              soff, 0);
 }
 // one lane's records of a factorization step: meta word + FAC_MAXC (a, b, c, -) address quads
 struct FacRec {
   uint32_t mt;
-  uint4 t[FAC_MAXC];
+  uint32_t a[FAC_MAXC], b[FAC_MAXC], c[FAC_MAXC];
 };
-__device__ __forceinline__ void load_fac(const uint32_t* step, int lane, FacRec& r) {
-  r.mt = step[lane];
-  const uint4* tp = reinterpret_cast<const uint4*>(step + 64) + lane;
+__device__ __forceinline__ void load_fac(Rsrc rs, int soff, uint32_t lane, FacRec& r) {
+  r.mt = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lane * 4u), soff, 0);
 #pragma unroll
-  for (int c = 0; c < FAC_MAXC; ++c) r.t[c] = tp[c * 64];
+  for (int c = 0; c < FAC_MAXC; ++c) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + 256 + c * 1024, soff, 0);
+    r.a[c] = q[0], r.b[c] = q[1], r.c[c] = q[2];
+  }
 }
 
-// straight-line dot products (two accumulators halve the dependent FMA chain).  All LDS reads are
+// straight-line dot product (two accumulators halve the dependent FMA chain).  All LDS reads are
 // forced in front of the FMAs (sched_group_barrier: 0x100 = DS read, 0x002 = VALU) so that they
 // overlap instead of paying one LDS round trip per term.
 template <int C>
-__device__ __forceinline__ double dot2(const double* v, const uint2* t) {
-  double x[C], y[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    x[c] = lds_ld(v, t[c].x);
-    y[c] = lds_ld(v, t[c].y);
-  }
-  __builtin_amdgcn_sched_group_barrier(0x100, 2 * C, 0);
-  __builtin_amdgcn_sched_group_barrier(0x002, 2 * C, 0);
-  double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    if (c & 1)
-      a1 = fma(x[c], y[c], a1);
-    else
-      a0 = fma(x[c], y[c], a0);
-  }
-  return a0 + a1;
-}
-template <int C>
-__device__ __forceinline__ double dot3(const double* v, const uint4* t) {
+__device__ __forceinline__ double dot3(const double* v, const FacRec& r) {
   double x[C], y[C], d[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    x[c] = lds_ld(v, t[c].x);
-    y[c] = lds_ld(v, t[c].y);
-    d[c] = lds_ld(v, t[c].z);
+    x[c] = lds_ld(v, r.a[c]);
+    y[c] = lds_ld(v, r.b[c]);
+    d[c] = lds_ld(v, r.c[c]);
   }
   __builtin_amdgcn_sched_group_barrier(0x100, 3 * C, 0);
   __builtin_amdgcn_sched_group_barrier(0x002, 3 * C, 0);
@@ -204,21 +217,33 @@ __device__ __forceinline__ double dot3(const double* v, const uint4* t) {
   return a0 + a1;
 }
 
-// One solve step: v[t] <- -sum_c v[a_c] * v[b_c].  Every lane stores: the lanes of a group hold
-// the group's bitwise-identical sum and store it to the task's slot, idle lanes store to their
-// own sink slot, so the store needs no branch.
+// One solve step.  Negated segment sums n_q = -(v[a_2q] v[b_2q] + v[a_2q+1] v[b_2q+1]) (the FMA
+// negate modifiers are free); output 0 is the lane's whole sum (FULL, then reduced over the lane
+// group), n0 + n1 (H0) or n0; output 2 is n2 + n3 (H1) or n2; outputs 1 and 3 are n1 and n3.
+// Output q is stored to target t_q; unused targets are the lane's sink slot and the lanes of a
+// group store the group's bitwise-identical sum to the same slot, so no store needs a branch.
+// Steps with fewer terms per lane read the ZERO slot in their unused term slots.
 __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(r.mt);
-  const uint32_t C = (m0 >> META_C_SHIFT) & 15u, glog = (m0 >> META_SGLOG_SHIFT) & 7u;
-  double acc;
-  if (C <= 2)
-    acc = dot2<2>(v, r.t);
-  else if (C <= 4)
-    acc = dot2<4>(v, r.t);
-  else
-    acc = dot2<8>(v, r.t);
-  acc = group_sum(acc, glog, (r.mt >> META_GLOG_SHIFT) & 7u);
-  lds_st(v, r.mt & META_TGT_MASK, -acc);
+  const uint32_t glog = (m0 >> META_SGLOG_SHIFT) & 7u;
+  const uint32_t gl = (r.mt >> META_GLOG_SHIFT) & 7u;
+  double x[8], y[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) x[c] = lds_ld(v, r.a[c]), y[c] = lds_ld(v, r.b[c]);
+  __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+  __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+  const double n0 = fma(-x[1], y[1], -(x[0] * y[0]));
+  const double n1 = fma(-x[3], y[3], -(x[2] * y[2]));
+  const double n2 = fma(-x[5], y[5], -(x[4] * y[4]));
+  const double n3 = fma(-x[7], y[7], -(x[6] * y[6]));
+  const double p01 = n0 + n1, p23 = n2 + n3;
+  double o0 = (r.mt & META_FULL) ? p01 + p23 : ((r.mt & META_H0) ? p01 : n0);
+  const double o2 = (r.mt & META_H1) ? p23 : n2;
+  o0 = group_sum(o0, glog, gl);
+  lds_st(v, r.t0, o0);
+  lds_st(v, r.t1, n1);
+  lds_st(v, r.t2, o2);
+  lds_st(v, r.t3, n3);
   LDS_FENCE();
 }
 // One factorization step: v[t] <- -sum_c v[a_c] v[b_c] v[c_c]; a D_j target also writes 1/D_j at
@@ -226,7 +251,7 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
 __device__ __forceinline__ void fac_step(const FacRec& r, double* v, uint32_t dshift) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(r.mt);
   const uint32_t C = (m0 >> META_C_SHIFT) & 15u, glog = (m0 >> META_SGLOG_SHIFT) & 7u;
-  double acc = C <= 2 ? dot3<2>(v, r.t) : dot3<4>(v, r.t);
+  double acc = C <= 2 ? dot3<2>(v, r) : dot3<4>(v, r);
   acc = group_sum(acc, glog, (r.mt >> META_GLOG_SHIFT) & 7u);
   if (r.mt & META_HEAD) {
     const uint32_t t = r.mt & META_TGT_MASK;
@@ -239,45 +264,83 @@ __device__ __forceinline__ void fac_step(const FacRec& r, double* v, uint32_t ds
 
 // Step loops.  Records (L2-resident, fixed stride) rotate through three register sets, so the
 // records of step s + 2 are in flight while steps s and s + 1 compute.
-template <typename Rec, typename Load, typename Step>
-__device__ __forceinline__ void run_steps(const uint32_t* tbl, int n, int lane, Load load, Step step) {
-  if (n <= 0) return;
-  auto at = [&](int s) { return tbl + (size_t)(s < n ? s : n - 1) * STEP_WORDS; };
-  Rec a, b, c;
-  load(at(0), lane, a);
-  load(at(1), lane, b);
-  load(at(2), lane, c);
+// Step loops.  Records (L2-resident, fixed stride) rotate through three register sets, so the
+// records of step s + 2 are in flight while steps s and s + 1 compute.  prefetch() issues the
+// first three steps' loads; callers issue it ahead of unrelated work to hide the L2 latency.
+template <typename Ops>
+struct Pipe {
+  typename Ops::Rec a, b, c;
+};
+template <typename Ops>
+__device__ __forceinline__ int step_off(int n, int s) {
+  return (s < n ? s : n - 1) * (Ops::STRIDE * 4);
+}
+template <typename Ops>
+__device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops>& p) {
+  // n >= 1 (checked at plan time); no branch here, so the vmcnt bookkeeping after it is exact
+  // the sets are issued in order (sched_barrier) so that the vmcnt wait for one set never
+  // includes a later one
+  __builtin_amdgcn_sched_barrier(0);
+  Ops::load(rs, step_off<Ops>(n, 0), lane, p.a);
+  __builtin_amdgcn_sched_barrier(0);
+  Ops::load(rs, step_off<Ops>(n, 1), lane, p.b);
+  __builtin_amdgcn_sched_barrier(0);
+  Ops::load(rs, step_off<Ops>(n, 2), lane, p.c);
+  __builtin_amdgcn_sched_barrier(0);
+}
+// The rotation is unrolled 12 steps deep: LLVM's waitcnt insertion merges states pessimistically
+// at a loop header (the first step after it would wait for all three sets), so the header is
+// reached at most once per ~12 steps.
+#define MPCQP_STEP(X)                                       \
+  ops.step(p.X);                                            \
+  if (++s >= n) break;                                      \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  Ops::load(rs, step_off<Ops>(n, s + 2), lane, p.X);        \
+  __builtin_amdgcn_sched_barrier(0);
+template <typename Ops>
+__device__ __forceinline__ void run_body(Rsrc rs, int n, uint32_t lane, const Ops& ops,
+                                         Pipe<Ops>& p) {
   int s = 0;
   for (;;) {
-    step(a);
-    if (++s >= n) break;
-    load(at(s + 2), lane, a);
-    step(b);
-    if (++s >= n) break;
-    load(at(s + 2), lane, b);
-    step(c);
-    if (++s >= n) break;
-    load(at(s + 2), lane, c);
+    MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
+    MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
+    MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
+    MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
   }
 }
-__device__ __forceinline__ void run_solve(const uint32_t* tbl, int nsteps, double* v, int lane) {
-  run_steps<SolveRec>(
-      tbl, nsteps, lane,
-      [](const uint32_t* st, int ln, SolveRec& r) { load_solve(st, ln, r); },
-      [v](const SolveRec& r) { solve_step(r, v); });
-}
+#undef MPCQP_STEP
+struct SolveOps {
+  typedef SolveRec Rec;
+  static constexpr int STRIDE = SOLVE_STEP_WORDS;
+  double* v;
+  __device__ __forceinline__ static void load(Rsrc rs, int soff, uint32_t lane, Rec& r) {
+    load_solve(rs, soff, lane, r);
+  }
+  __device__ __forceinline__ void step(const Rec& r) const { solve_step(r, v); }
+};
+struct FacOps {
+  typedef FacRec Rec;
+  static constexpr int STRIDE = FAC_STEP_WORDS;
+  double* v;
+  uint32_t dshift;
+  __device__ __forceinline__ static void load(Rsrc rs, int soff, uint32_t lane, Rec& r) {
+    load_fac(rs, soff, lane, r);
+  }
+  __device__ __forceinline__ void step(const Rec& r) const { fac_step(r, v, dshift); }
+};
 __device__ __forceinline__ void run_fac(const uint32_t* tbl, int nsteps, double* v, int lane,
                                         uint32_t dshift) {
-  run_steps<FacRec>(
-      tbl, nsteps, lane, [](const uint32_t* st, int ln, FacRec& r) { load_fac(st, ln, r); },
-      [v, dshift](const FacRec& r) { fac_step(r, v, dshift); });
+  Pipe<FacOps> pp;
+  const Rsrc rs = table_rsrc(tbl, nsteps, FAC_STEP_WORDS);
+  prefetch(rs, nsteps, (uint32_t)lane, pp);
+  run_body(rs, nsteps, (uint32_t)lane, FacOps{v, dshift}, pp);
 }
 
 // numeric LDL': U = L D and D by levels, L = U / D (flat pass), then the block-inverse tail
 __device__ __forceinline__ void run_factor(const KParams& p, double* v, int lane) {
   const DevPlan& P = p.pl;
   const uint32_t dshift = (uint32_t)(P.DINV - P.W) * 8u;
-  if (P.nfac > 0) run_fac(P.fac, P.nfac, v, lane, dshift);
+  run_fac(P.fac, P.nfac, v, lane, dshift);
   LDS_FENCE();
 #pragma unroll 4
   for (int k = lane; k < P.nnzL; k += 64) v[P.LX + k] *= v[P.Lcol[k]];
@@ -749,10 +812,18 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   const Slab sb = slab_of(P, scr);
   Inst<RN, RM> S;
   const int hs = p.has_state[inst];
+#ifdef MPCQP_TIMING
+  unsigned long long tacc[T_NSLOT] = {};
+#endif
+  T_BEGIN(t_sc);
   scale_problem<RN, RM>(p, inst, hs, S, sb, v, lane);
+  T_END(T_SCALE, t_sc);
   S.rho = (hs != 0) ? p.rho_state[inst] : dmind(dmaxd(p.s.rho, RHO_MIN), RHO_MAX);
   set_rho(S);
+  T_BEGIN(t_f0);
   assemble_and_factor<RN, RM>(p, sb, v, lane, S);
+  T_END(T_FACTOR, t_f0);
+  T_COUNT(T_NFACT);
 
   // ---------------- warm start
   const bool warm = p.s.warm_start && hs != 0;
@@ -824,7 +895,14 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   bool can_check = false;
   double dx[RN], dy[RM];
   Resid<RN, RM> R;
+  Pipe<SolveOps> sp;
+  const SolveOps sops{v};
+  const Rsrc rs_fwd = table_rsrc(P.fwd, P.nfwd, SOLVE_STEP_WORDS);
+  const Rsrc rs_bwd = table_rsrc(P.bwd, P.nbwd, SOLVE_STEP_WORDS);
   for (iter = 1; iter <= p.s.max_iter; ++iter) {
+    T_COUNT(T_ITERS);
+    T_BEGIN(t_v0);
+    prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);  // lands while the right-hand side is formed
     double xp[RN], zp[RM], bz[RM];
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
 #pragma unroll
@@ -841,10 +919,19 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       if (i < m) v[wsz[r] + coff] = bz[r];
     }
     LDS_FENCE();
-    run_solve(P.fwd, P.nfwd, v, lane);
+    T_END(T_VEC, t_v0);
+    T_BEGIN(t_fw);
+    run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
+    T_END(T_FWD, t_fw);
+    T_BEGIN(t_v1);
+    prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
     for (int k = lane; k < P.nk; k += 64) v[P.CACC + k] = v[P.W + k] * v[P.DINV + k];
     LDS_FENCE();
-    run_solve(P.bwd, P.nbwd, v, lane);
+    T_END(T_VEC, t_v1);
+    T_BEGIN(t_bw);
+    run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
+    T_END(T_BWD, t_bw);
+    T_BEGIN(t_v2);
     // x, z, y updates (auxil.c update_x / update_z / update_y)
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
@@ -865,6 +952,8 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       S.y[r] = S.y[r] + dy[r];
     }
     LDS_FENCE();
+    T_END(T_VEC, t_v2);
+    T_BEGIN(t_ck);
     can_check = chk && (iter % chk == 0);
     const bool adapt = p.s.adaptive_rho && ar_int && (iter % ar_int == 0);
 #ifndef EXP_NOCHECK
@@ -887,10 +976,19 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         set_rho(S);
         rho_updates++;
         LDS_FENCE();
+        T_BEGIN(t_f1);
         assemble_and_factor<RN, RM>(p, sb, v, lane, S);
+#ifdef MPCQP_TIMING
+        const unsigned long long dt_f1 = __builtin_amdgcn_s_memtime() - t_f1;
+        tacc[T_FACTOR] += dt_f1;
+        tacc[T_CHECK] -= dt_f1;  // the check slot excludes the refactorization
+#endif
+        T_COUNT(T_NFACT);
       }
     }
+    T_END(T_CHECK, t_ck);
   }
+  T_BEGIN(t_tl);
   if (!can_check) {
     iter = iter - 1;
     compute_residuals(p, S, R, sb, v, lane);
@@ -946,6 +1044,11 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       p.Ecls[(size_t)inst * m + i] = sb.E[i];
     }
   }
+  T_END(T_TAIL, t_tl);
+#ifdef MPCQP_TIMING
+  if (lane == 0 && p.timing)
+    for (int k = 0; k < T_NSLOT; ++k) atomicAdd(p.timing + k, tacc[k]);
+#endif
   if (lane == 0) {
     p.rho_state[inst] = S.rho;
     p.has_state[inst] = 1;
@@ -1039,6 +1142,7 @@ struct mpcqp_handle {
   int32_t* has_state = nullptr;
   double* scratch = nullptr;
   unsigned int* counter = nullptr;
+  unsigned long long* timing = nullptr;  // MPCQP_TIMING builds
   bool has_data = false;
   int grid = 0, lds_bytes = 0, waves_per_cu = 0;
   kernel_fn kern = nullptr;
@@ -1110,6 +1214,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     return fail(MPCQP_E_UNSUPPORTED, e);
   }
   const Plan& pl = h->plan;
+  if (pl.nfac < 1 || pl.nfwd < 1 || pl.nbwd < 1) {
+    delete h;
+    return fail(MPCQP_E_UNSUPPORTED, "internal: empty schedule");
+  }
   h->kern = select_kernel(pl.n, pl.m);
   if (!h->kern) {
     delete h;
@@ -1278,11 +1386,21 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   if (info) p.info = *info;
   p.scratch = h->scratch;
   p.counter = h->counter;
+  p.timing = h->timing;
   HIPCHK(hipMemsetAsync(h->counter, 0, 64, h->stream));
   hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(64), h->lds_bytes, h->stream, p);
   HIPCHK(hipGetLastError());
   return 0;
 }
+
+#ifdef MPCQP_TIMING
+// diagnostic builds only (not part of include/mpcqp.h): device buffer of T_NSLOT uint64 counters
+int mpcqp_debug_timing(mpcqp_handle* h, unsigned long long* dev_buf) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  h->timing = dev_buf;
+  return 0;
+}
+#endif
 
 int mpcqp_data_buffers(mpcqp_handle* h, double** Ax, double** l, double** u) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");

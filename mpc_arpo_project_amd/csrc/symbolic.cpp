@@ -52,13 +52,10 @@ struct Task {
   std::vector<std::array<int, 3>> terms;  // LDS slots; solve terms use the first two
 };
 
-// Pack one level's tasks into fixed-stride 64-lane steps appended to tbl (see symbolic.hpp).
-// Returns the number of steps.  In-place tasks get the term (-1) * v[t] (times 1 for the
-// factorization); a task with more terms than one step holds is split into chunks that run in
-// consecutive rounds of steps, every chunk after the first in place.
-int pack_level(const std::vector<Task>& tasks, bool fac, const Plan& pl, std::vector<uint32_t>& tbl) {
-  const int maxc = fac ? FAC_MAXC : SOLVE_MAXC;
-  const int cap = 64 * maxc;
+// In-place tasks get the term (-1) * v[t] (times 1 for the factorization); a task with more terms
+// than `cap` is split into chunks that run in consecutive rounds of steps, every chunk after the
+// first in place.
+std::vector<std::vector<Task>> make_rounds(const std::vector<Task>& tasks, int cap, const Plan& pl) {
   std::vector<std::vector<Task>> rounds;
   for (const Task& t : tasks) {
     size_t pos = 0;
@@ -75,13 +72,21 @@ int pack_level(const std::vector<Task>& tasks, bool fac, const Plan& pl, std::ve
       rounds[r].push_back(std::move(c));
     }
   }
+  return rounds;
+}
+
+// Pack one factorization level into fixed-stride 64-lane steps appended to tbl (see
+// symbolic.hpp): a task gets an aligned group of lanes, only the group head stores.  Returns the
+// number of steps.
+int pack_fac_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<uint32_t>& tbl) {
+  const int maxc = FAC_MAXC;
   struct Placed {
     const Task* t;
     int g, glog, c;
   };
   const uint32_t zb = (uint32_t)pl.ZERO * 8u;
   int nsteps = 0;
-  for (const auto& rt : rounds) {
+  for (const auto& rt : make_rounds(tasks, 64 * maxc, pl)) {
     std::vector<Placed> pv;
     for (const Task& t : rt) {
       const int nt = (int)t.terms.size();
@@ -108,13 +113,10 @@ int pack_level(const std::vector<Task>& tasks, bool fac, const Plan& pl, std::ve
         i++;
       }
       const size_t base = tbl.size();
-      tbl.resize(base + STEP_WORDS, zb);
+      tbl.resize(base + FAC_STEP_WORDS, zb);
       uint32_t* st = tbl.data() + base;
-      // idle lanes of a solve step store to their own sink slot (the device stores
-      // unconditionally); group lanes other than the head store the same value as the head
       for (int l = 0; l < 64; ++l)
-        st[l] = ((uint32_t)C << META_C_SHIFT) | ((uint32_t)glog << META_SGLOG_SHIFT) |
-                (fac ? 0u : (uint32_t)(pl.SINK + l) * 8u);
+        st[l] = ((uint32_t)C << META_C_SHIFT) | ((uint32_t)glog << META_SGLOG_SHIFT);
       for (auto& pr : in) {
         const int off = pr.first;
         const Placed* p = pr.second;
@@ -122,22 +124,139 @@ int pack_level(const std::vector<Task>& tasks, bool fac, const Plan& pl, std::ve
           uint32_t mt = ((uint32_t)p->glog << META_GLOG_SHIFT) | ((uint32_t)p->t->target * 8u);
           if (r == 0) mt |= META_HEAD;
           if (p->t->isD) mt |= META_ISD;
-          st[off + r] = (st[off + r] & ~META_TGT_MASK) | mt;
+          st[off + r] |= mt;
         }
         const auto& tv = p->t->terms;
         for (size_t q = 0; q < tv.size(); q++) {
           const int lane = off + (int)(q % p->g), c = (int)(q / p->g);
-          if (fac) {
-            uint32_t* w = st + 64 + c * 256 + lane * 4;
-            w[0] = (uint32_t)tv[q][0] * 8u, w[1] = (uint32_t)tv[q][1] * 8u;
-            w[2] = (uint32_t)tv[q][2] * 8u;
-          } else {
-            uint32_t* w = st + 64 + c * 128 + lane * 2;
-            w[0] = (uint32_t)tv[q][0] * 8u, w[1] = (uint32_t)tv[q][1] * 8u;
-          }
+          uint32_t* w = st + 64 + c * 256 + lane * 4;
+          w[0] = (uint32_t)tv[q][0] * 8u, w[1] = (uint32_t)tv[q][1] * 8u;
+          w[2] = (uint32_t)tv[q][2] * 8u;
         }
       }
       nsteps++;
+    }
+  }
+  return nsteps;
+}
+
+// Pack one solve level into fixed-stride 64-lane steps appended to tbl.  A lane's 8 term slots are
+// 4 two-term segments (quarters): tasks of <= 2 terms take a quarter, <= 4 a half, <= 8 a whole
+// lane, longer ones an aligned group of whole lanes (META_FULL).  Every lane stores all four
+// segment outputs (unused ones to its sink slot), so stores need no branch.
+int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<uint32_t>& tbl) {
+  struct Item {
+    const Task* t;
+    int units, g, glog;  // quarters needed (1, 2, 4) or lanes (g) for groups
+  };
+  const uint32_t zb = (uint32_t)pl.ZERO * 8u;
+  int nsteps = 0;
+  for (const auto& rt : make_rounds(tasks, 64 * SOLVE_MAXC, pl)) {
+    std::vector<Item> items;
+    for (const Task& t : rt) {
+      const int nt = (int)t.terms.size();
+      Item it{&t, 0, 1, 0};
+      if (nt <= 2) {
+        it.units = 1;
+      } else if (nt <= 4) {
+        it.units = 2;
+      } else {
+        it.units = 4;
+        while (it.g < 64 && (nt + it.g - 1) / it.g > SOLVE_MAXC) it.g *= 2, it.glog++;
+      }
+      items.push_back(it);
+    }
+    std::stable_sort(items.begin(), items.end(), [](const Item& x, const Item& y) {
+      if (x.g != y.g) return x.g > y.g;
+      return x.units > y.units;
+    });
+    std::vector<Item> pending = items;
+    while (!pending.empty()) {
+      // per lane: occupied quarters (bit mask), task per quarter
+      uint32_t occ[64] = {};
+      const Task* qt[64][4] = {};
+      uint32_t flags[64] = {};
+      int lglog[64] = {};
+      std::vector<Item> deferred;
+      int C = 0, sglog = 0;
+      for (const Item& it : pending) {
+        bool placed = false;
+        if (it.units == 4) {
+          for (int off = 0; off + it.g <= 64 && !placed; off += it.g) {
+            bool free = true;
+            for (int r = 0; r < it.g; ++r) free = free && occ[off + r] == 0;
+            if (!free) continue;
+            const int nt = (int)it.t->terms.size();
+            for (int r = 0; r < it.g; ++r) {
+              occ[off + r] = 15u;
+              qt[off + r][0] = it.t;
+              flags[off + r] = META_FULL;
+              lglog[off + r] = it.glog;
+            }
+            C = std::max(C, (nt + it.g - 1) / it.g);
+            sglog = std::max(sglog, it.glog);
+            placed = true;
+          }
+        } else {
+          const uint32_t need = it.units == 2 ? 3u : 1u;
+          const int stride = it.units;
+          // first fit, preferring lanes already in use (keeps whole lanes free for later items)
+          for (int pass = 0; pass < 2 && !placed; ++pass)
+            for (int l = 0; l < 64 && !placed; ++l) {
+              if ((pass == 0) != (occ[l] != 0)) continue;
+              for (int q = 0; q < 4 && !placed; q += stride) {
+                if (occ[l] & (need << q)) continue;
+                occ[l] |= need << q;
+                qt[l][q] = it.t;
+                if (it.units == 2) flags[l] |= q == 0 ? META_H0 : META_H1;
+                C = std::max(C, 2 * q + (int)it.t->terms.size());
+                placed = true;
+              }
+            }
+        }
+        if (!placed) deferred.push_back(it);
+      }
+      C = C <= 2 ? 2 : (C <= 4 ? 4 : 8);
+      const size_t base = tbl.size();
+      tbl.resize(base + SOLVE_STEP_WORDS, zb);
+      uint32_t* terms = tbl.data() + base;
+      uint32_t* tg = terms + SOLVE_TERM_WORDS;
+      uint32_t* meta = tg + 64 * 4;
+      // term slot c of lane l: segment row c / 2, word 2 * (c % 2) of the lane's quad
+      auto slot = [&](int c, int l) { return terms + (c / 2) * 256 + l * 4 + (c % 2) * 2; };
+      for (int l = 0; l < 64; ++l) {
+        meta[l] = ((uint32_t)C << META_C_SHIFT) | ((uint32_t)sglog << META_SGLOG_SHIFT) | flags[l] |
+                  ((uint32_t)lglog[l] << META_GLOG_SHIFT);
+        const uint32_t sink = (uint32_t)(pl.SINK + l) * 8u;
+        for (int q = 0; q < 4; ++q) tg[l * 4 + q] = qt[l][q] ? (uint32_t)qt[l][q]->target * 8u : sink;
+      }
+      // terms: group tasks strided over their lanes, others from the first slot of their segment
+      std::vector<const Task*> done;
+      for (int l = 0; l < 64; ++l)
+        for (int q = 0; q < 4; ++q) {
+          const Task* t = qt[l][q];
+          if (!t) continue;
+          if (flags[l] & META_FULL) {
+            if (std::find(done.begin(), done.end(), t) != done.end()) continue;
+            done.push_back(t);
+            int g = 0;  // lanes of the group (consecutive, starting here)
+            while (l + g < 64 && qt[l + g][0] == t) g++;
+            for (size_t k = 0; k < t->terms.size(); ++k) {
+              const int lane = l + (int)(k % g), c = (int)(k / g);
+              slot(c, lane)[0] = (uint32_t)t->terms[k][0] * 8u;
+              slot(c, lane)[1] = (uint32_t)t->terms[k][1] * 8u;
+            }
+          } else {
+            for (size_t k = 0; k < t->terms.size(); ++k) {
+              const int c = 2 * q + (int)k;
+              slot(c, l)[0] = (uint32_t)t->terms[k][0] * 8u;
+              slot(c, l)[1] = (uint32_t)t->terms[k][1] * 8u;
+            }
+          }
+        }
+      // a group's non-first lanes store the same value to the same target: no sink needed
+      nsteps++;
+      pending.swap(deferred);
     }
   }
   return nsteps;
@@ -456,7 +575,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
         if (!t.terms.empty()) tasks.push_back(std::move(t));
       }
     }
-    pl.nfac += pack_level(tasks, true, pl, pl.fac);
+    pl.nfac += pack_fac_level(tasks, pl, pl.fac);
   }
   pl.Lcol.resize(pl.nnzL);
   for (int j = 0; j < nk; j++)
@@ -488,7 +607,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
           tasks.push_back(std::move(t));
         }
       }
-      pl.ntail += pack_level(tasks, true, pl, pl.tail);
+      pl.ntail += pack_fac_level(tasks, pl, pl.tail);
     }
     std::vector<Task> tasks;
     for (int r = 0; r < nk; r++) {
@@ -517,11 +636,12 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
         tasks.push_back(std::move(t));
       }
     }
-    pl.ntail += pack_level(tasks, true, pl, pl.tail);
+    pl.ntail += pack_fac_level(tasks, pl, pl.tail);
   }
-  // ---- forward solve (input C = rhs, output W): per block k
-  //   W_r = sum_{r2 in reach(r) U {r}} M_{r r2} C_{r2} - sum_{x in block k-1} G_{r x} W_x
-  //   C_r -= sum_{x in block k-1} L_{r x} W_x          for rows r beyond block k
+  // ---- forward solve (input C = rhs, output W): level k
+  //   W_r = sum_{r2 in reach(r) U {r}} M_{r r2} C_{r2} - sum_{x in block k-1} G_{r x} W_x   (r in block k)
+  //   C_r -= sum_{x in blocks <= k-1} L_{r x} W_x                 (r in block k+1: one merged task,
+  //                                                                  just in time for level k+1)
   for (int k = 0; k < T; k++) {
     std::vector<Task> tasks;
     for (int r = bs(k); r < be(k); r++) {
@@ -532,20 +652,20 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
       for (int x : gpat[r]) t.terms.push_back({gslot(r, x), pl.W + x, 0});
       tasks.push_back(std::move(t));
     }
-    if (k >= 1)
-      for (int r = be(k); r < nk; r++) {
+    if (k + 1 < T)
+      for (int r = bs(k + 1); r < be(k + 1); r++) {
         Task t;
         t.target = pl.CACC + r;
         t.inplace = true;
         for (int x : lrow[r])
-          if (x >= bs(k - 1) && x < be(k - 1)) t.terms.push_back({pl.LX + lpos(r, x), pl.W + x, 0});
+          if (x < bs(k)) t.terms.push_back({pl.LX + lpos(r, x), pl.W + x, 0});
         if (!t.terms.empty()) tasks.push_back(std::move(t));
       }
-    pl.nfwd += pack_level(tasks, false, pl, pl.fwd);
+    pl.nfwd += pack_solve_level(tasks, pl, pl.fwd);
   }
-  // ---- backward solve (input C = D^-1 W, output W): blocks in reverse
+  // ---- backward solve (input C = D^-1 W, output W): blocks in reverse, level k
   //   W_r = sum_{r2: r in reach(r2) or r2 == r} M_{r2 r} C_{r2} - sum_{z in block k+1} G'_{r z} W_z
-  //   C_r -= sum_{z in block k+1} L_{z r} W_z          for rows r before block k
+  //   C_r -= sum_{z in blocks >= k+1} L_{z r} W_z                 (r in block k-1, merged)
   for (int k = T - 1; k >= 0; k--) {
     std::vector<Task> tasks;
     for (int r = bs(k); r < be(k); r++) {
@@ -556,16 +676,16 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
       for (int z : gppat[r]) t.terms.push_back({gpslot(r, z), pl.W + z, 0});
       tasks.push_back(std::move(t));
     }
-    if (k + 1 < T)
-      for (int r = 0; r < bs(k); r++) {
+    if (k >= 1)
+      for (int r = bs(k - 1); r < be(k - 1); r++) {
         Task t;
         t.target = pl.CACC + r;
         t.inplace = true;
         for (int z : lcol[r])
-          if (z >= bs(k + 1) && z < be(k + 1)) t.terms.push_back({pl.LX + lpos(z, r), pl.W + z, 0});
+          if (z >= be(k)) t.terms.push_back({pl.LX + lpos(z, r), pl.W + z, 0});
         if (!t.terms.empty()) tasks.push_back(std::move(t));
       }
-    pl.nbwd += pack_level(tasks, false, pl, pl.bwd);
+    pl.nbwd += pack_solve_level(tasks, pl, pl.bwd);
   }
   pl.levels_fwd = T;
   pl.levels_bwd = T;

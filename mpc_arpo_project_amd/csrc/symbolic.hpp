@@ -28,16 +28,26 @@ namespace mpcqp {
 
 constexpr int SOLVE_MAXC = 8;   // terms per lane of a solve step
 constexpr int FAC_MAXC = 4;     // terms per lane of a factorization step
-constexpr int STEP_WORDS = 64 + 64 * 2 * SOLVE_MAXC;
-static_assert(STEP_WORDS == 64 + 64 * 4 * FAC_MAXC, "solve and factor steps share a stride");
+// factorization step: meta[64] | FAC_MAXC rows of 64 (a, b, c, 0) quads
+constexpr int FAC_STEP_WORDS = 64 + 64 * 4 * FAC_MAXC;
+// solve step: SOLVE_MAXC / 2 rows of 64 segment quads (a0, b0, a1, b1) | 64 target quads
+// (t0, t1, t2, t3) | meta[64]
+constexpr int SOLVE_TERM_WORDS = 64 * 2 * SOLVE_MAXC;
+constexpr int SOLVE_STEP_WORDS = SOLVE_TERM_WORDS + 64 * 4 + 64;
 
 // meta word: per-lane fields, then the step-wide C and glog (identical in every lane)
-constexpr uint32_t META_TGT_MASK = 0x1ffffu;  // LDS byte address of the target
+constexpr uint32_t META_TGT_MASK = 0x1ffffu;  // factorization: LDS byte address of the target
 constexpr int META_GLOG_SHIFT = 17;           // 3 bits: this lane's group size log2
 constexpr uint32_t META_HEAD = 1u << 20;
 constexpr uint32_t META_ISD = 1u << 21;       // factorization: target is D_j -> also write 1/D_j
 constexpr int META_C_SHIFT = 22;              // 4 bits: terms per lane in this step
 constexpr int META_SGLOG_SHIFT = 26;          // 3 bits: widest group log2 in this step
+// solve steps: a lane's 8 term slots are 4 two-term segments s0..s3 whose sums go to targets
+// t0..t3; FULL merges all four into t0 (one task, possibly spanning a lane group), H0 merges
+// s0 + s1 into t0, H1 merges s2 + s3 into t2.  Unused targets are the lane's sink slot.
+constexpr uint32_t META_FULL = 1u << 29;
+constexpr uint32_t META_H0 = 1u << 30;
+constexpr uint32_t META_H1 = 1u << 31;
 
 struct Plan {
   int n = 0, m = 0, nk = 0, nnzP = 0, nnzA = 0, nnzL = 0;

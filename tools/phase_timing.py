@@ -1,0 +1,81 @@
+"""Per-phase cycle breakdown of the QP kernel on the bench workload (diagnostic build).
+
+    python tools/phase_timing.py build            # here: hipcc -DMPCQP_TIMING -> tools/libmpcqp_timing.so
+    python tools/phase_timing.py run [B] [steps]  # GPU box: warm closed loop, prints cycles per phase
+
+The timing build stamps s_memtime around scaling, factorization, forward / backward solves, the
+vector work of an ADMM iteration, and the checks (engine.hip, MPCQP_TIMING).  Cycles are s_memtime
+ticks (shader clock) summed over all instances of the timed steps.
+"""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "tools", "libmpcqp_timing.so")
+SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact"]
+
+
+def build(extra=()):
+    csrc = os.path.join(REPO, "mpc_arpo_project_amd", "csrc")
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+           "-DMPCQP_TIMING", *extra, os.path.join(csrc, "engine.hip"),
+           os.path.join(csrc, "closed_loop.hip"), os.path.join(csrc, "symbolic.cpp"), "-o", LIB]
+    subprocess.check_call(cmd)
+
+
+def run(B=65536, steps=5, warmup=3, nx=20):
+    os.environ["MPCQP_LIBRARY"] = LIB
+    sys.path.insert(0, REPO)
+    import ctypes as C
+
+    import torch
+    from mpc_arpo_project_amd import _lib, qp_model, scenarios
+    from mpc_arpo_project_amd.closed_loop import BatchClosedLoop
+
+    L = _lib.lib()
+    L.mpcqp_debug_timing.argtypes = [C.c_void_p, C.c_void_p]
+    sim, mpc, fail, deb = scenarios.radial_scenario(Nx=nx)
+    prob = qp_model.build_problem(sim, mpc, fail, deb)
+    X = scenarios.sample_estimates(B, seed=20250328)[:, :4].copy()
+    X[:, 2:4] = 0.0
+    cl = BatchClosedLoop(prob, X, device=torch.device("cuda", 0), eps_abs=1e-4, eps_rel=1e-4)
+    for _ in range(warmup):
+        cl.step()
+    buf = torch.zeros(len(SLOTS), dtype=torch.int64, device="cuda")
+    L.mpcqp_debug_timing(cl.qp._h, C.c_void_p(buf.data_ptr()))
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kt = 0.0
+    for _ in range(steps):
+        ev0.record(cl.qp.stream)
+        r = cl.qp.solve_async()
+        ev1.record(cl.qp.stream)
+        cl.step_after_solve(r)
+        torch.cuda.synchronize()
+        kt += ev0.elapsed_time(ev1)
+    t = dict(zip(SLOTS, buf.cpu().tolist()))
+    n_inst = B * steps
+    iters = t["iters"]
+    sched = cl.qp.schedule_info()
+    out = {"B": B, "steps": steps, "kernel_ms_per_launch": kt / steps,
+           "iters_per_solve": iters / n_inst, "factorizations_per_solve": t["nfact"] / n_inst,
+           "cycles_per_solve": {k: t[k] / n_inst for k in SLOTS[:7]},
+           "cycles_per_iter": {k: t[k] / iters for k in ("fwd", "bwd", "vec", "check")},
+           "cycles_per_factorization": t["factor"] / max(t["nfact"], 1),
+           "cycles_per_solve_step": {"fwd": t["fwd"] / iters / sched["fwd_steps"],
+                                     "bwd": t["bwd"] / iters / sched["bwd_steps"]},
+           "cycles_per_factor_step": t["factor"] / max(t["nfact"], 1) / sched["fac_steps"],
+           "schedule": sched}
+    tot = sum(t[k] for k in SLOTS[:7])
+    out["share"] = {k: t[k] / tot for k in SLOTS[:7]}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(sys.argv[2:])
+    else:
+        args = [int(a) for a in sys.argv[2:]]
+        run(*args)
