@@ -41,7 +41,14 @@ using namespace mpcqp;
 namespace {
 
 // ------------------------------------------------------------------------------------- device
+struct EllDev {
+  const uint16_t *src, *in;
+  int K[ELL_MAXR], off[ELL_MAXR];
+  int total, nlong;
+  int long_out[ELL_MAXLONG], long_off[ELL_MAXLONG], long_cnt[ELL_MAXLONG];
+};
 struct DevPlan {
+  EllDev eA, eAt, eP;  // residual mat-vecs (symbolic.hpp Ell)
   const uint32_t *fac, *tail, *fwd, *bwd;  // fixed-stride step records (symbolic.hpp)
   int nfac, ntail, nfwd, nbwd;
   const uint16_t* Lcol;    // DINV slot of each L entry's column
@@ -70,7 +77,7 @@ struct KParams {
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
 // s_memtime deltas accumulated per wave in SGPRs, added to p.timing at the end of each instance.
-enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_NSLOT };
+enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_NSLOT };
 #ifdef MPCQP_TIMING
 #define T_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define T_END(slot, v) tacc[slot] += __builtin_amdgcn_s_memtime() - (v)
@@ -89,17 +96,32 @@ enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT
 __device__ __forceinline__ double dmaxd(double a, double b) { return a > b ? a : b; }
 __device__ __forceinline__ double dmind(double a, double b) { return a < b ? a : b; }
 
-// xor-butterfly reductions: every lane ends with the bitwise-identical result (each stage adds
-// the same two operands in both partner lanes; fp addition is commutative)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                          __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+// Wave all-reductions: DPP butterflies inside each 16-lane row (partners exchange and combine the
+// same two operands, so every lane of a row holds the bitwise-identical row result), then the four
+// row results combined as wave-uniform values.
 __device__ __forceinline__ double wave_max(double x) {
-#pragma unroll
-  for (int k = 1; k < 64; k <<= 1) x = dmaxd(x, __shfl_xor(x, k));
-  return x;
+  x = dmaxd(x, dpp_d<0xB1>(x));   // quad_perm [1,0,3,2]
+  x = dmaxd(x, dpp_d<0x4E>(x));   // quad_perm [2,3,0,1]
+  x = dmaxd(x, dpp_d<0x141>(x));  // row_half_mirror
+  x = dmaxd(x, dpp_d<0x140>(x));  // row_mirror
+  return dmaxd(dmaxd(readlane_d(x, 0), readlane_d(x, 16)), dmaxd(readlane_d(x, 32), readlane_d(x, 48)));
 }
 __device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-  for (int k = 1; k < 64; k <<= 1) x += __shfl_xor(x, k);
-  return x;
+  x += dpp_d<0xB1>(x);
+  x += dpp_d<0x4E>(x);
+  x += dpp_d<0x141>(x);
+  x += dpp_d<0x140>(x);
+  return (readlane_d(x, 0) + readlane_d(x, 16)) + (readlane_d(x, 32) + readlane_d(x, 48));
 }
 __device__ __forceinline__ double limit_scaling(double d) {
   d = d < MIN_SCALING ? 1.0 : d;
@@ -115,15 +137,9 @@ __device__ __forceinline__ double lds_ld(const double*, uint32_t a) {
 }
 __device__ __forceinline__ void lds_st(double*, uint32_t a, double x) { *(lds_double*)(size_t)a = x; }
 
-// 64-bit cross-lane moves for the group butterflies: DPP inside rows of 16 lanes (quad_perm xor 1,
-// xor 2, row_half_mirror, row_mirror pair the partners of an aligned group exactly like an xor
-// butterfly does for an all-reduce), ds_bpermute beyond that.
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double x) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, false);
-  return __hiloint2double(hi, lo);
-}
+// Group butterflies: DPP inside rows of 16 lanes (quad_perm xor 1, xor 2, row_half_mirror,
+// row_mirror pair the partners of an aligned group exactly like an xor butterfly does for an
+// all-reduce), ds_bpermute beyond that.
 // all-reduce of acc over this lane's aligned group of 2^gl lanes (glog = widest group of the step,
 // wave-uniform); stages beyond the step's widest group are skipped by uniform branches
 __device__ __forceinline__ double group_sum(double acc, uint32_t glog, uint32_t gl) {
@@ -239,11 +255,15 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
   const double p01 = n0 + n1, p23 = n2 + n3;
   double o0 = (r.mt & META_FULL) ? p01 + p23 : ((r.mt & META_H0) ? p01 : n0);
   const double o2 = (r.mt & META_H1) ? p23 : n2;
+#ifndef EXP_NO_LADDER  // timing ablations (tools/phase_timing.py builds only; results wrong)
   o0 = group_sum(o0, glog, gl);
+#endif
   lds_st(v, r.t0, o0);
+#ifndef EXP_NO_STORE123
   lds_st(v, r.t1, n1);
   lds_st(v, r.t2, o2);
   lds_st(v, r.t3, n3);
+#endif
   LDS_FENCE();
 }
 // One factorization step: v[t] <- -sum_c v[a_c] v[b_c] v[c_c]; a D_j target also writes 1/D_j at
@@ -367,7 +387,11 @@ struct Inst {
 // per-wave scratch slab layout (doubles)
 struct Slab {
   double *Ps, *As, *D, *Dinv, *E, *Einv;
+  double *vA, *vAt, *vP;  // scaled values in the residual ELL orders
 };
+__device__ __forceinline__ size_t slab_doubles(const DevPlan& P) {
+  return (size_t)P.nnzP + P.nnzA + 2 * P.n + 2 * P.m + P.eA.total + P.eAt.total + P.eP.total;
+}
 __device__ __forceinline__ Slab slab_of(const DevPlan& P, double* scr) {
   Slab s;
   s.Ps = scr;
@@ -376,7 +400,60 @@ __device__ __forceinline__ Slab slab_of(const DevPlan& P, double* scr) {
   s.Dinv = s.D + P.n;
   s.E = s.Dinv + P.n;
   s.Einv = s.E + P.m;
+  s.vA = s.Einv + P.m;
+  s.vAt = s.vA + P.eA.total;
+  s.vP = s.vAt + P.eAt.total;
   return s;
+}
+// residual mat-vec out[r] = sum_k val[off_r + 64 k + lane] * in[idx[...]] for every slot r of
+// the instance (terms in order).  All value and index loads are issued before the first use.
+template <int R, int KMAX>
+__device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const double* in,
+                                       double (&out)[R], int lane) {
+  double a[R][KMAX];
+  uint32_t ix[R][KMAX];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (e.K[r] == 0) continue;  // slot beyond the instance (wave-uniform)
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int t = e.off[r] + 64 * k + lane;
+      a[r][k] = val[t];
+      ix[r][k] = e.in[t];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    double s = 0.0;
+    if (e.K[r] != 0) {
+      double b[KMAX];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) b[k] = in[ix[r][k]];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) s += a[r][k] * b[k];
+    }
+    out[r] = s;
+  }
+  // outputs with more than KMAX terms: wave-cooperative sums
+  for (int L = 0; L < e.nlong; ++L) {
+    double s = 0.0;
+    for (int t = lane; t < e.long_cnt[L]; t += 64) {
+      const int q = e.long_off[L] + t;
+      s += val[q] * in[e.in[q]];
+    }
+    s = wave_sum(s);
+    const int o = e.long_out[L];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (o == lane + 64 * r) out[r] = s;
+  }
+}
+// gather the scaled values (scaling overlay in LDS) into the slab's ELL copies
+__device__ __forceinline__ void ell_park(const EllDev& e, double* dst, const double* v, int lane) {
+  for (int t = lane; t < e.total; t += 64) {
+    const uint32_t src = e.src[t];
+    dst[t] = src != 0xffffu ? v[src] : 0.0;
+  }
 }
 
 template <int RN, int RM>
@@ -469,27 +546,20 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   }
   LDS_FENCE();
   double pr = 0.0, dr = 0.0;
+  ell_mv<RM, ELL_KA>(P.eA, sb.vA, xb, R.Ax, lane);  // padding terms are 0 * x
+  ell_mv<RN, ELL_KP>(P.eP, sb.vP, xb, R.Px, lane);
+  ell_mv<RN, ELL_KAT>(P.eAt, sb.vAt, yb, R.Aty, lane);
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
-    double s = 0.0;
-    if (i < m) {
-      for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) s += sb.As[P.Ark[q]] * xb[P.Arj[q]];
-      pr = dmaxd(pr, fabs(sb.Einv[i] * (s - S.z[r])));
-    }
-    R.Ax[r] = s;
+    if (i < m) pr = dmaxd(pr, fabs(sb.Einv[i] * (R.Ax[r] - S.z[r])));
+    if (i >= m) R.Ax[r] = 0.0;
   }
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
-    double sp = 0.0, sa = 0.0;
-    if (j < n) {
-      for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) sp += sb.Ps[P.Psk[e]] * xb[P.Pso[e]];
-      for (int k = P.Ap[j]; k < P.Ap[j + 1]; ++k) sa += sb.As[k] * yb[P.Ai[k]];
-      dr = dmaxd(dr, fabs(sb.Dinv[j] * ((S.q[r] + sp) + sa)));
-    }
-    R.Px[r] = sp;
-    R.Aty[r] = sa;
+    if (j < n) dr = dmaxd(dr, fabs(sb.Dinv[j] * ((S.q[r] + R.Px[r]) + R.Aty[r])));
+    if (j >= n) R.Px[r] = 0.0, R.Aty[r] = 0.0;
   }
   S.pri_res = wave_max(pr);
   S.dua_res = S.cinv * wave_max(dr);
@@ -798,9 +868,12 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
       sb.Dinv[j] = 1. / D[r];
     }
   }
-  // park scaled P, A for residuals / refactorization (per-wave slab, L2-resident)
+  // park scaled P, A for residuals / refactorization (per-wave slab)
   for (int k = lane; k < P.nnzP; k += 64) sb.Ps[k] = v[P.S_P + k];
   for (int k = lane; k < P.nnzA; k += 64) sb.As[k] = v[P.S_A + k];
+  ell_park(P.eA, sb.vA, v, lane);
+  ell_park(P.eAt, sb.vAt, v, lane);
+  ell_park(P.eP, sb.vP, v, lane);
   LDS_FENCE();
 }
 
@@ -891,6 +964,8 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   const int chk = p.s.check_termination;
   int ar_int = p.s.adaptive_rho_interval;
   if (p.s.adaptive_rho && ar_int == 0) ar_int = chk ? 4 * chk : 100;
+  if (!p.s.adaptive_rho) ar_int = 0;
+  int chk_left = chk, ar_left = ar_int;  // iterations to the next check / rho adaptation
   int status = MPCQP_UNSOLVED, iter = 0, rho_updates = 0;
   bool can_check = false;
   double dx[RN], dy[RM];
@@ -954,20 +1029,30 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     LDS_FENCE();
     T_END(T_VEC, t_v2);
     T_BEGIN(t_ck);
-    can_check = chk && (iter % chk == 0);
-    const bool adapt = p.s.adaptive_rho && ar_int && (iter % ar_int == 0);
+    can_check = chk && --chk_left == 0;  // iter % chk == 0
+    if (can_check) chk_left = chk;
+    const bool adapt = ar_int && --ar_left == 0;  // iter % ar_int == 0
+    if (adapt) ar_left = ar_int;
 #ifndef EXP_NOCHECK
-    if (can_check || adapt) compute_residuals(p, S, R, sb, v, lane);
+    if (can_check || adapt) {
+      T_BEGIN(t_rs);
+      compute_residuals(p, S, R, sb, v, lane);
+      T_END(T_RESID, t_rs);
+      T_COUNT(T_NCHK);
+    }
 #endif
     if (can_check) {
 #ifdef EXP_NOCHECK
       if (iter > 100) break;
       continue;
 #endif
+      T_BEGIN(t_tm);
       status = check_termination(p, S, R, dy, dx, sb, v, lane, false);
+      T_END(T_TERM, t_tm);
       if (status != 0) break;
       status = MPCQP_UNSOLVED;
     }
+    T_BEGIN(t_ad);
     if (adapt) {
       const double rho_new = rho_estimate(p, S, R, lane);
       if (rho_new > S.rho * p.s.adaptive_rho_tolerance ||
@@ -982,10 +1067,12 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         const unsigned long long dt_f1 = __builtin_amdgcn_s_memtime() - t_f1;
         tacc[T_FACTOR] += dt_f1;
         tacc[T_CHECK] -= dt_f1;  // the check slot excludes the refactorization
+        tacc[T_ADAPT] -= dt_f1;
 #endif
         T_COUNT(T_NFACT);
       }
     }
+    T_END(T_ADAPT, t_ad);
     T_END(T_CHECK, t_ck);
   }
   T_BEGIN(t_tl);
@@ -1069,8 +1156,7 @@ __global__ void __launch_bounds__(64) qp_batch_kernel(KParams p) {
   const int lane = (int)threadIdx.x;
   if ((uint32_t)(uintptr_t)lds != 0u) __builtin_trap();  // schedule byte addresses assume base 0
   double* v = lds;
-  const size_t slab = (size_t)(p.pl.nnzP + p.pl.nnzA + 2 * p.pl.n + 2 * p.pl.m);
-  double* scr = p.scratch + (size_t)blockIdx.x * slab;
+  double* scr = p.scratch + (size_t)blockIdx.x * slab_doubles(p.pl);
   for (;;) {
     unsigned int inst = 0;
     if (lane == 0) inst = atomicAdd(p.counter, 1u);
@@ -1235,7 +1321,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
          o_Ark = push_blob(blob, pl.Ark), o_Arj = push_blob(blob, pl.Arj),
          o_Pi = push_blob(blob, pl.Pi), o_Pc = push_blob(blob, pl.Pcol),
          o_Psp = push_blob(blob, pl.Psp), o_Psk = push_blob(blob, pl.Psk),
-         o_Pso = push_blob(blob, pl.Pso);
+         o_Pso = push_blob(blob, pl.Pso), o_eAs = push_blob(blob, pl.ellA.src),
+         o_eAi = push_blob(blob, pl.ellA.in), o_eTs = push_blob(blob, pl.ellAt.src),
+         o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
+         o_ePi = push_blob(blob, pl.ellP.in);
   auto cleanup_fail = [&](int code, const std::string& msg) {
     mpcqp_destroy(h);
     return fail(code, msg);
@@ -1259,6 +1348,16 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   dp.Pi = (const uint16_t*)(b + o_Pi), dp.Pcol = (const uint16_t*)(b + o_Pc);
   dp.Psp = (const uint16_t*)(b + o_Psp), dp.Psk = (const uint16_t*)(b + o_Psk);
   dp.Pso = (const uint16_t*)(b + o_Pso);
+  auto ell = [&](const Ell& e, size_t os, size_t oi, EllDev& d) {
+    d.src = (const uint16_t*)(b + os), d.in = (const uint16_t*)(b + oi), d.total = e.total;
+    for (int r = 0; r < ELL_MAXR; ++r) d.K[r] = e.K[r], d.off[r] = e.off[r];
+    d.nlong = e.nlong;
+    for (int q = 0; q < ELL_MAXLONG; ++q)
+      d.long_out[q] = e.long_out[q], d.long_off[q] = e.long_off[q], d.long_cnt[q] = e.long_cnt[q];
+  };
+  ell(pl.ellA, o_eAs, o_eAi, dp.eA);
+  ell(pl.ellAt, o_eTs, o_eTi, dp.eAt);
+  ell(pl.ellP, o_ePs, o_ePi, dp.eP);
   dp.inst_doubles = (pl.LDS_N + 1) & ~1;
   dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
   dp.nnzL = pl.nnzL;
@@ -1298,7 +1397,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
             hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid *
-                                       (pl.nnzP + pl.nnzA + 2 * pl.n + 2 * pl.m)) ==
+                                       ((size_t)pl.nnzP + pl.nnzA + 2 * pl.n + 2 * pl.m +
+                                        pl.ellA.total + pl.ellAt.total + pl.ellP.total)) ==
                 hipSuccess &&
             hipMalloc(&h->counter, 64) == hipSuccess;
   if (!ok) return cleanup_fail(MPCQP_E_HIP, "hipMalloc(batch buffers)");

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <array>
 #include <numeric>
 #include <unordered_map>
@@ -145,6 +146,11 @@ int pack_fac_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<u
 // lane, longer ones an aligned group of whole lanes (META_FULL).  Every lane stores all four
 // segment outputs (unused ones to its sink slot), so stores need no branch.
 int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<uint32_t>& tbl) {
+  if (getenv("MPCQP_DUMP_TASKS")) {
+    fprintf(stderr, "level:");
+    for (const Task& t : tasks) fprintf(stderr, " %zu", t.terms.size() + (t.inplace ? 1 : 0));
+    fprintf(stderr, "\n");
+  }
   struct Item {
     const Task* t;
     int units, g, glog;  // quarters needed (1, 2, 4) or lanes (g) for groups
@@ -260,6 +266,42 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
     }
   }
   return nsteps;
+}
+
+// padded per-slot ELL of `count` outputs; terms(e) lists (src, in) in summation order
+template <typename F>
+bool make_ell(int count, int kmax, F terms, Ell& e) {
+  e = Ell();
+  e.kmax = kmax;
+  e.R = (count + 63) / 64;
+  if (e.R > ELL_MAXR) return false;
+  std::vector<std::vector<std::pair<int, int>>> t(count);
+  for (int i = 0; i < count; ++i) t[i] = terms(i);
+  for (int r = 0; r < e.R; ++r) {
+    e.K[r] = kmax;
+    e.off[r] = e.total;
+    e.total += 64 * kmax;
+  }
+  e.src.assign(e.total, 0xffff);
+  e.in.assign(e.total, 0);
+  for (int i = 0; i < count; ++i) {
+    const int r = i / 64, l = i % 64;
+    if ((int)t[i].size() > kmax) {
+      if (e.nlong >= ELL_MAXLONG) return false;
+      e.long_out[e.nlong] = i;
+      e.long_off[e.nlong] = (int)e.src.size();
+      e.long_cnt[e.nlong] = (int)t[i].size();
+      e.nlong++;
+      for (auto& pr : t[i]) e.src.push_back((uint16_t)pr.first), e.in.push_back((uint16_t)pr.second);
+      continue;
+    }
+    for (size_t k = 0; k < t[i].size(); ++k) {
+      e.src[e.off[r] + 64 * k + l] = (uint16_t)t[i][k].first;
+      e.in[e.off[r] + 64 * k + l] = (uint16_t)t[i][k].second;
+    }
+  }
+  e.total = (int)e.src.size();
+  return true;
 }
 
 }  // namespace
@@ -726,6 +768,26 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   for (int j = 0; j < n; j++) {
     pl.Psp[j + 1] = (uint16_t)(pl.Psp[j] + sym[j].size());
     for (auto& e : sym[j]) pl.Psk.push_back((uint16_t)e.first), pl.Pso.push_back((uint16_t)e.second);
+  }
+  // ---- residual mat-vecs (same term order as the CSR / CSC / symmetric traversals above)
+  bool ok = make_ell(m, ELL_KA, [&](int i) {
+    std::vector<std::pair<int, int>> t;
+    for (int q = rc[i]; q < rc[i + 1]; ++q) t.push_back({pl.S_A + pl.Ark[q], pl.Arj[q]});
+    return t;
+  }, pl.ellA);
+  ok = ok && make_ell(n, ELL_KAT, [&](int j) {
+    std::vector<std::pair<int, int>> t;
+    for (int k = Ap[j]; k < Ap[j + 1]; ++k) t.push_back({pl.S_A + k, Ai[k]});
+    return t;
+  }, pl.ellAt);
+  ok = ok && make_ell(n, ELL_KP, [&](int j) {
+    std::vector<std::pair<int, int>> t;
+    for (auto& e : sym[j]) t.push_back({pl.S_P + e.first, e.second});
+    return t;
+  }, pl.ellP);
+  if (!ok) {
+    pl.error = "problem too large for the residual layout";
+    return false;
   }
   return true;
 }

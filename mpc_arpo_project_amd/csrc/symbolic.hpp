@@ -49,6 +49,26 @@ constexpr uint32_t META_FULL = 1u << 29;
 constexpr uint32_t META_H0 = 1u << 30;
 constexpr uint32_t META_H1 = 1u << 31;
 
+// Sparse mat-vec in padded per-slot ELL form for the residual checks: output element e sits on
+// lane e % 64, register slot r = e / 64; every used slot has exactly KMAX terms per lane (compile-
+// time width, zero padding), term k of lane l at off[r] + 64 k + l: src = LDS slot of the scaled
+// value in the scaling overlay (0xffff = padding), in = index of the input element.  Outputs with
+// more than KMAX terms are "long": their terms are listed separately (long_off/long_cnt into the
+// tail of src/in) and summed cooperatively by the whole wave.  The per-instance values are gathered
+// into the slab in this order once per scaling, so a mat-vec issues all its loads back to back.
+constexpr int ELL_MAXR = 16;
+constexpr int ELL_MAXLONG = 8;
+constexpr int ELL_KA = 8;    // rows of A
+constexpr int ELL_KAT = 12;  // columns of A
+constexpr int ELL_KP = 4;    // symmetric rows of P
+struct Ell {
+  int R = 0, total = 0, kmax = 0;
+  int K[ELL_MAXR] = {}, off[ELL_MAXR] = {};  // K[r] = kmax for used slots, 0 otherwise
+  int nlong = 0;
+  int long_out[ELL_MAXLONG] = {}, long_off[ELL_MAXLONG] = {}, long_cnt[ELL_MAXLONG] = {};
+  std::vector<uint16_t> src, in;
+};
+
 struct Plan {
   int n = 0, m = 0, nk = 0, nnzP = 0, nnzA = 0, nnzL = 0;
   std::vector<int32_t> perm, pinv, Lp, Li, etree;
@@ -79,6 +99,7 @@ struct Plan {
   std::vector<uint16_t> Pi, Pcol;      // upper CSC of P: row / column of each entry
   std::vector<uint16_t> Psp, Psk, Pso; // symmetric traversal: per column j the P entries of
                                        // column j and row j, their position and the other index
+  Ell ellA, ellAt, ellP;  // A x (rows of A), A' y (columns), P x (symmetric rows of P)
   int levels_fwd = 0, levels_bwd = 0;
   std::string error;
 };

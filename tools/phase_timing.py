@@ -13,8 +13,8 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(REPO, "tools", "libmpcqp_timing.so")
-SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact"]
+LIB = os.environ.get("MPCQP_TIMING_LIB") or os.path.join(REPO, "tools", "libmpcqp_timing.so")
+SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact", "resid", "term", "nchk", "adapt"]
 
 
 def build(extra=()):
@@ -64,6 +64,10 @@ def run(B=65536, steps=5, warmup=3, nx=20):
            "cycles_per_solve": {k: t[k] / n_inst for k in SLOTS[:7]},
            "cycles_per_iter": {k: t[k] / iters for k in ("fwd", "bwd", "vec", "check")},
            "cycles_per_factorization": t["factor"] / max(t["nfact"], 1),
+           "cycles_per_check": {"resid": t["resid"] / max(t["nchk"], 1),
+                                "term": t["term"] / max(t["nchk"], 1),
+                                "adapt": t["adapt"] / max(t["nchk"], 1),
+                                "check_total": t["check"] / max(t["nchk"], 1)},
            "cycles_per_solve_step": {"fwd": t["fwd"] / iters / sched["fwd_steps"],
                                      "bwd": t["bwd"] / iters / sched["bwd_steps"]},
            "cycles_per_factor_step": t["factor"] / max(t["nfact"], 1) / sched["fac_steps"],
