@@ -54,6 +54,10 @@ extern "C" {
 #define MPCQP_E_UNSUPPORTED (-3)  /* structure or setting this build cannot handle */
 #define MPCQP_E_NODATA (-4)       /* solve before set_data */
 
+/* linear-system engines (mpcqp_engine_kind) */
+#define MPCQP_ENGINE_KKT 0    /* blocked level-scheduled LDL' of the quasi-definite KKT matrix */
+#define MPCQP_ENGINE_DENSE 1  /* explicit inverse of P + sigma I + A' diag(rho) A (n <= 128) */
+
 /* OSQP 0.6 status_val values */
 #define MPCQP_SOLVED 1
 #define MPCQP_SOLVED_INACCURATE 2
@@ -136,6 +140,10 @@ int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int
  * triangular solves, LDS bytes per instance and resident waves (instances in flight) per CU. */
 int mpcqp_schedule_info(const mpcqp_handle *h, int32_t *fac_steps, int32_t *fwd_steps,
                         int32_t *bwd_steps, int32_t *lds_bytes, int32_t *waves_per_cu);
+/* Which linear-system engine the handle runs: the dense-inverse engine is chosen for n <= 128 and
+ * m <= 256, the KKT engine otherwise; environment variable MPCQP_ENGINE=kkt|dense (read by
+ * mpcqp_create) forces one.  Both give OSQP 0.6's iterates up to rounding. */
+int mpcqp_engine_kind(const mpcqp_handle *h, int32_t *kind);
 /* Host-only symbolic analysis (no HIP call; usable without a GPU): KKT ordering, L pattern and
  * schedule statistics for a structure.  perm [n+m], Lp [n+m+1] may be NULL; Li is written only
  * when non-NULL and *nnzL (in) >= the true count.  stats (may be NULL) receives

@@ -19,7 +19,7 @@ EXPORTED = (
     "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",
     "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
     "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
-    "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version",
+    "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind",
     "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
 )
 
@@ -99,6 +99,7 @@ def lib():
     L.mpcqp_warm_start.argtypes = [vp, dp, dp]
     L.mpcqp_solve.argtypes = [vp, dp, dp, C.POINTER(Info)]
     L.mpcqp_dims.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
+    L.mpcqp_engine_kind.argtypes = [vp, i32p]
     L.mpcqp_copy_data.argtypes = [vp, dp, dp, dp]
     L.mpcqp_data_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
     L.mpcqp_schedule_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]

@@ -26,6 +26,8 @@
 
 #include "../../include/mpcqp.h"
 #include "symbolic.hpp"
+#include "dense.hpp"
+#include "dense_dev.hpp"
 
 using namespace mpcqp;
 
@@ -1229,6 +1231,7 @@ struct mpcqp_handle {
   double* scratch = nullptr;
   unsigned int* counter = nullptr;
   unsigned long long* timing = nullptr;  // MPCQP_TIMING builds
+  DenseEngine* dense = nullptr;          // dense-inverse engine (dense.hip) when selected
   bool has_data = false;
   int grid = 0, lds_bytes = 0, waves_per_cu = 0;
   kernel_fn kern = nullptr;
@@ -1304,86 +1307,113 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, "internal: empty schedule");
   }
-  h->kern = select_kernel(pl.n, pl.m);
-  if (!h->kern) {
+  // engine: the KKT engine by default; MPCQP_ENGINE=dense selects the dense-inverse engine for
+  // small problems (dense.hpp).  Measured on the bench workload the dense engine is
+  // slower (one instance per CU) and its explicit inverse less exact on infeasible instances,
+  // so it is opt-in.
+  const char* eng = getenv("MPCQP_ENGINE");
+  const bool force_dense = eng && strcmp(eng, "dense") == 0;
+  if (force_dense && !dense_supported(pl.n, pl.m)) {
     delete h;
-    return fail(MPCQP_E_UNSUPPORTED, "problem dimensions exceed the instantiated kernels");
+    return fail(MPCQP_E_UNSUPPORTED, "MPCQP_ENGINE=dense: n <= 128 and m <= 256 required");
   }
-  // structure blob
-  std::vector<char> blob;
-  size_t o_fac = push_blob(blob, pl.fac), o_tail = push_blob(blob, pl.tail),
-         o_fwd = push_blob(blob, pl.fwd), o_bwd = push_blob(blob, pl.bwd),
-         o_Lc = push_blob(blob, pl.Lcol), o_sP = push_blob(blob, pl.slotP),
-         o_sA = push_blob(blob, pl.slotA), o_sR = push_blob(blob, pl.slotRho),
-         o_sS = push_blob(blob, pl.slotSig), o_wx = push_blob(blob, pl.wsx),
-         o_wz = push_blob(blob, pl.wsz), o_Ap = push_blob(blob, pl.Ap), o_Ai = push_blob(blob, pl.Ai),
-         o_Ac = push_blob(blob, pl.Acol), o_Arp = push_blob(blob, pl.Arp),
-         o_Ark = push_blob(blob, pl.Ark), o_Arj = push_blob(blob, pl.Arj),
-         o_Pi = push_blob(blob, pl.Pi), o_Pc = push_blob(blob, pl.Pcol),
-         o_Psp = push_blob(blob, pl.Psp), o_Psk = push_blob(blob, pl.Psk),
-         o_Pso = push_blob(blob, pl.Pso), o_eAs = push_blob(blob, pl.ellA.src),
-         o_eAi = push_blob(blob, pl.ellA.in), o_eTs = push_blob(blob, pl.ellAt.src),
-         o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
-         o_ePi = push_blob(blob, pl.ellP.in);
+  if (force_dense) {
+    DenseInputs di{st->n, st->m, batch, st->Pp, st->Pi, st->Ap, st->Ai};
+    std::string err;
+    const int rc = dense_create(di, &h->dense, err);
+    if (rc != 0 && (force_dense || rc != MPCQP_E_UNSUPPORTED)) {
+      delete h;
+      return fail(rc, err);
+    }
+    if (rc != 0 && getenv("MPCQP_DEBUG"))
+      fprintf(stderr, "mpcqp: dense engine not used (%s); KKT engine\n", err.c_str());
+    if (h->dense) {  // (a structure the dense engine cannot lay out falls back to the KKT engine)
+      dense_info(h->dense, &h->grid, &h->lds_bytes, &h->waves_per_cu);
+      h->waves_per_cu *= DENSE_THREADS / 64;
+    }
+  }
   auto cleanup_fail = [&](int code, const std::string& msg) {
     mpcqp_destroy(h);
     return fail(code, msg);
   };
-  if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
-    return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
-  if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
-    return cleanup_fail(MPCQP_E_HIP, "hipMemcpy(structure)");
-  char* b = h->d_blob;
-  DevPlan& dp = h->dp;
-  dp.fac = (const uint32_t*)(b + o_fac), dp.tail = (const uint32_t*)(b + o_tail);
-  dp.fwd = (const uint32_t*)(b + o_fwd), dp.bwd = (const uint32_t*)(b + o_bwd);
-  dp.nfac = pl.nfac, dp.ntail = pl.ntail, dp.nfwd = pl.nfwd, dp.nbwd = pl.nbwd;
-  dp.Lcol = (const uint16_t*)(b + o_Lc);
-  dp.slotP = (const uint16_t*)(b + o_sP), dp.slotA = (const uint16_t*)(b + o_sA);
-  dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
-  dp.wsx = (const uint16_t*)(b + o_wx), dp.wsz = (const uint16_t*)(b + o_wz);
-  dp.Ap = (const uint16_t*)(b + o_Ap), dp.Ai = (const uint16_t*)(b + o_Ai);
-  dp.Acol = (const uint16_t*)(b + o_Ac), dp.Arp = (const uint16_t*)(b + o_Arp);
-  dp.Ark = (const uint16_t*)(b + o_Ark), dp.Arj = (const uint16_t*)(b + o_Arj);
-  dp.Pi = (const uint16_t*)(b + o_Pi), dp.Pcol = (const uint16_t*)(b + o_Pc);
-  dp.Psp = (const uint16_t*)(b + o_Psp), dp.Psk = (const uint16_t*)(b + o_Psk);
-  dp.Pso = (const uint16_t*)(b + o_Pso);
-  auto ell = [&](const Ell& e, size_t os, size_t oi, EllDev& d) {
-    d.src = (const uint16_t*)(b + os), d.in = (const uint16_t*)(b + oi), d.total = e.total;
-    for (int r = 0; r < ELL_MAXR; ++r) d.K[r] = e.K[r], d.off[r] = e.off[r];
-    d.nlong = e.nlong;
-    for (int q = 0; q < ELL_MAXLONG; ++q)
-      d.long_out[q] = e.long_out[q], d.long_off[q] = e.long_off[q], d.long_cnt[q] = e.long_cnt[q];
-  };
-  ell(pl.ellA, o_eAs, o_eAi, dp.eA);
-  ell(pl.ellAt, o_eTs, o_eTi, dp.eAt);
-  ell(pl.ellP, o_ePs, o_ePi, dp.eP);
-  dp.inst_doubles = (pl.LDS_N + 1) & ~1;
-  dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
-  dp.nnzL = pl.nnzL;
-  dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.CACC = pl.CACC, dp.ZERO = pl.ZERO;
-  dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N;
-  dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
+  if (!h->dense) {
+    h->kern = select_kernel(pl.n, pl.m);
+    if (!h->kern) {
+      delete h;
+      return fail(MPCQP_E_UNSUPPORTED, "problem dimensions exceed the instantiated kernels");
+    }
+    // structure blob
+    std::vector<char> blob;
+    size_t o_fac = push_blob(blob, pl.fac), o_tail = push_blob(blob, pl.tail),
+           o_fwd = push_blob(blob, pl.fwd), o_bwd = push_blob(blob, pl.bwd),
+           o_Lc = push_blob(blob, pl.Lcol), o_sP = push_blob(blob, pl.slotP),
+           o_sA = push_blob(blob, pl.slotA), o_sR = push_blob(blob, pl.slotRho),
+           o_sS = push_blob(blob, pl.slotSig), o_wx = push_blob(blob, pl.wsx),
+           o_wz = push_blob(blob, pl.wsz), o_Ap = push_blob(blob, pl.Ap), o_Ai = push_blob(blob, pl.Ai),
+           o_Ac = push_blob(blob, pl.Acol), o_Arp = push_blob(blob, pl.Arp),
+           o_Ark = push_blob(blob, pl.Ark), o_Arj = push_blob(blob, pl.Arj),
+           o_Pi = push_blob(blob, pl.Pi), o_Pc = push_blob(blob, pl.Pcol),
+           o_Psp = push_blob(blob, pl.Psp), o_Psk = push_blob(blob, pl.Psk),
+           o_Pso = push_blob(blob, pl.Pso), o_eAs = push_blob(blob, pl.ellA.src),
+           o_eAi = push_blob(blob, pl.ellA.in), o_eTs = push_blob(blob, pl.ellAt.src),
+           o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
+           o_ePi = push_blob(blob, pl.ellP.in);
+    if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
+      return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
+    if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup_fail(MPCQP_E_HIP, "hipMemcpy(structure)");
+    char* b = h->d_blob;
+    DevPlan& dp = h->dp;
+    dp.fac = (const uint32_t*)(b + o_fac), dp.tail = (const uint32_t*)(b + o_tail);
+    dp.fwd = (const uint32_t*)(b + o_fwd), dp.bwd = (const uint32_t*)(b + o_bwd);
+    dp.nfac = pl.nfac, dp.ntail = pl.ntail, dp.nfwd = pl.nfwd, dp.nbwd = pl.nbwd;
+    dp.Lcol = (const uint16_t*)(b + o_Lc);
+    dp.slotP = (const uint16_t*)(b + o_sP), dp.slotA = (const uint16_t*)(b + o_sA);
+    dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
+    dp.wsx = (const uint16_t*)(b + o_wx), dp.wsz = (const uint16_t*)(b + o_wz);
+    dp.Ap = (const uint16_t*)(b + o_Ap), dp.Ai = (const uint16_t*)(b + o_Ai);
+    dp.Acol = (const uint16_t*)(b + o_Ac), dp.Arp = (const uint16_t*)(b + o_Arp);
+    dp.Ark = (const uint16_t*)(b + o_Ark), dp.Arj = (const uint16_t*)(b + o_Arj);
+    dp.Pi = (const uint16_t*)(b + o_Pi), dp.Pcol = (const uint16_t*)(b + o_Pc);
+    dp.Psp = (const uint16_t*)(b + o_Psp), dp.Psk = (const uint16_t*)(b + o_Psk);
+    dp.Pso = (const uint16_t*)(b + o_Pso);
+    auto ell = [&](const Ell& e, size_t os, size_t oi, EllDev& d) {
+      d.src = (const uint16_t*)(b + os), d.in = (const uint16_t*)(b + oi), d.total = e.total;
+      for (int r = 0; r < ELL_MAXR; ++r) d.K[r] = e.K[r], d.off[r] = e.off[r];
+      d.nlong = e.nlong;
+      for (int q = 0; q < ELL_MAXLONG; ++q)
+        d.long_out[q] = e.long_out[q], d.long_off[q] = e.long_off[q], d.long_cnt[q] = e.long_cnt[q];
+    };
+    ell(pl.ellA, o_eAs, o_eAi, dp.eA);
+    ell(pl.ellAt, o_eTs, o_eTi, dp.eAt);
+    ell(pl.ellP, o_ePs, o_ePi, dp.eP);
+    dp.inst_doubles = (pl.LDS_N + 1) & ~1;
+    dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
+    dp.nnzL = pl.nnzL;
+    dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.CACC = pl.CACC, dp.ZERO = pl.ZERO;
+    dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N;
+    dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
 
-  // occupancy (LDS image and VGPRs) -> persistent grid
-  int dev = 0, ncu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return cleanup_fail(MPCQP_E_HIP, "hipGetDevice");
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return cleanup_fail(MPCQP_E_HIP, "hipDeviceGetAttribute");
-  const int inst_bytes = dp.inst_doubles * 8;
-  const int lds_cap = 160 * 1024;
-  if (inst_bytes > lds_cap)
-    return cleanup_fail(MPCQP_E_UNSUPPORTED, "instance image exceeds the LDS of a CU");
-  if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          lds_cap) != hipSuccess)
-    return cleanup_fail(MPCQP_E_HIP, "hipFuncSetAttribute");
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, 64, inst_bytes) !=
-          hipSuccess || nb <= 0)
-    return cleanup_fail(MPCQP_E_UNSUPPORTED, "kernel does not fit on a CU (LDS/VGPR)");
-  h->waves_per_cu = nb;
-  h->lds_bytes = inst_bytes;
-  h->grid = std::min(batch, nb * ncu);
+    // occupancy (LDS image and VGPRs) -> persistent grid
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return cleanup_fail(MPCQP_E_HIP, "hipGetDevice");
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return cleanup_fail(MPCQP_E_HIP, "hipDeviceGetAttribute");
+    const int inst_bytes = dp.inst_doubles * 8;
+    const int lds_cap = 160 * 1024;
+    if (inst_bytes > lds_cap)
+      return cleanup_fail(MPCQP_E_UNSUPPORTED, "instance image exceeds the LDS of a CU");
+    if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds_cap) != hipSuccess)
+      return cleanup_fail(MPCQP_E_HIP, "hipFuncSetAttribute");
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, 64, inst_bytes) !=
+            hipSuccess || nb <= 0)
+      return cleanup_fail(MPCQP_E_UNSUPPORTED, "kernel does not fit on a CU (LDS/VGPR)");
+    h->waves_per_cu = nb;
+    h->lds_bytes = inst_bytes;
+    h->grid = std::min(batch, nb * ncu);
+  }
   const size_t Bz = (size_t)batch;
   bool ok = hipMalloc(&h->Px, sizeof(double) * std::max(1, pl.nnzP)) == hipSuccess &&
             hipMalloc(&h->q, sizeof(double) * pl.n) == hipSuccess &&
@@ -1396,10 +1426,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->Ecls, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
-            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid *
+            (h->dense || hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid *
                                        ((size_t)pl.nnzP + pl.nnzA + 2 * pl.n + 2 * pl.m +
                                         pl.ellA.total + pl.ellAt.total + pl.ellP.total)) ==
-                hipSuccess &&
+                hipSuccess) &&
             hipMalloc(&h->counter, 64) == hipSuccess;
   if (!ok) return cleanup_fail(MPCQP_E_HIP, "hipMalloc(batch buffers)");
   if (hipMemset(h->has_state, 0, sizeof(int32_t) * Bz) != hipSuccess)
@@ -1410,6 +1440,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
 
 int mpcqp_destroy(mpcqp_handle* h) {
   if (!h) return 0;
+  dense_destroy(h->dense);
   void* bufs[] = {h->d_blob, h->Px, h->q,    h->Ax,        h->l,       h->u,      h->xs,
                   h->zs,     h->ys, h->Ecls, h->rho, h->has_state, h->scratch, h->counter};
   for (void* b : bufs)
@@ -1488,6 +1519,19 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   p.counter = h->counter;
   p.timing = h->timing;
   HIPCHK(hipMemsetAsync(h->counter, 0, 64, h->stream));
+  if (h->dense) {
+    DenseSolveArgs a{};
+    a.s = h->set, a.B = h->B;
+    a.Px = h->Px, a.q = h->q, a.Ax = h->Ax, a.l = h->l, a.u = h->u;
+    a.xs = h->xs, a.zs = h->zs, a.ys = h->ys, a.rho_state = h->rho, a.Ecls = h->Ecls;
+    a.has_state = h->has_state, a.x_out = x, a.y_out = y;
+    if (info) a.info = *info;
+    a.counter = h->counter;
+    a.timing = h->timing;
+    if (dense_solve(h->dense, a, h->stream) != 0)
+      return fail(MPCQP_E_HIP, std::string("dense kernel launch: ") + hipGetErrorString(hipGetLastError()));
+    return 0;
+  }
   hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(64), h->lds_bytes, h->stream, p);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1539,11 +1583,17 @@ int mpcqp_dims(const mpcqp_handle* h, int32_t* n, int32_t* m, int32_t* nnzP, int
 int mpcqp_schedule_info(const mpcqp_handle* h, int32_t* fac, int32_t* fwd, int32_t* bwd,
                         int32_t* lds, int32_t* wpc) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");
-  if (fac) *fac = (int32_t)(h->plan.nfac + h->plan.ntail);
-  if (fwd) *fwd = (int32_t)h->plan.nfwd;
-  if (bwd) *bwd = (int32_t)h->plan.nbwd;
+  if (fac) *fac = h->dense ? 0 : (int32_t)(h->plan.nfac + h->plan.ntail);
+  if (fwd) *fwd = h->dense ? 0 : (int32_t)h->plan.nfwd;
+  if (bwd) *bwd = h->dense ? 0 : (int32_t)h->plan.nbwd;
   if (lds) *lds = h->lds_bytes;
   if (wpc) *wpc = h->waves_per_cu;
+  return 0;
+}
+
+int mpcqp_engine_kind(const mpcqp_handle* h, int32_t* kind) {
+  if (!h || !kind) return fail(MPCQP_E_INVALID, "null argument");
+  *kind = h->dense ? MPCQP_ENGINE_DENSE : MPCQP_ENGINE_KKT;
   return 0;
 }
 

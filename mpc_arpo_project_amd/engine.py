@@ -198,8 +198,11 @@ class BatchQP:
         v = [C.c_int32() for _ in range(5)]
         check(_lib.lib().mpcqp_schedule_info(self._h, *[C.byref(x) for x in v]),
               "mpcqp_schedule_info")
-        return dict(fac_steps=v[0].value, fwd_steps=v[1].value, bwd_steps=v[2].value,
-                    lds_bytes=v[3].value, waves_per_cu=v[4].value)
+        k = C.c_int32()
+        check(_lib.lib().mpcqp_engine_kind(self._h, C.byref(k)), "mpcqp_engine_kind")
+        return dict(engine="dense" if k.value == 1 else "kkt", fac_steps=v[0].value,
+                    fwd_steps=v[1].value, bwd_steps=v[2].value, lds_bytes=v[3].value,
+                    waves_per_cu=v[4].value)
 
     def dims(self):
         v = [C.c_int32() for _ in range(5)]

@@ -142,3 +142,28 @@ def test_osqp_compat_errors(prob20):
     res = s.solve()
     assert res.info.status == "solved"
     assert torch.cuda.is_available()
+
+
+def test_dense_engine_opt_in(golden, monkeypatch):
+    """MPCQP_ENGINE=dense: the dense-inverse engine (explicit M^-1, dense.hip) takes the same ADMM
+    steps up to the inverse's rounding: statuses of the fixture set equal the oracle's, iteration
+    counts agree on nearly all instances, u0 within 1e-6 on instances both solve"""
+    from conftest import problem
+
+    prob = problem(20, False)
+    d = golden("batch_n20")
+    monkeypatch.setenv("MPCQP_ENGINE", "dense")
+    st = dict(eps_abs=1e-4, eps_rel=1e-4)
+    qp = BatchQP(prob.P, prob.A, batch=d["Ax"].shape[0], **st)
+    assert qp.schedule_info()["engine"] == "dense"
+    qp.set_data(q=prob.q, Ax=d["Ax"], l=d["l"], u=d["u"])
+    r = qp.solve()
+    xo, yo, so, io = orc.batch_solve(prob.P, prob.q, prob.A, d["Ax"], d["l"], d["u"], nthreads=8, **st)
+    sg, ig, xg = r.status.cpu().numpy(), r.iter.cpu().numpy(), r.x.cpu().numpy()
+    assert np.array_equal(sg, so), (sg, so)
+    assert np.mean(ig == io) >= 0.9, (ig, io)
+    ok = (so == 1) & (sg == 1)
+    sl = prob.u0_slice
+    assert np.max(np.abs(xg[ok][:, sl] - xo[ok][:, sl])) < 1e-6
+    monkeypatch.delenv("MPCQP_ENGINE")
+    assert BatchQP(prob.P, prob.A, batch=4, **st).schedule_info()["engine"] == "kkt"
