@@ -104,7 +104,7 @@ def main():
     ap.add_argument("--nx", type=int, default=20)
     ap.add_argument("--eps", type=float, default=1e-4)
     ap.add_argument("--seed", type=int, default=20250328)
-    ap.add_argument("--cpu-sample", type=int, default=8192)
+    ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

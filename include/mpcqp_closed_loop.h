@@ -5,8 +5,16 @@
  *   mpcqp_cl_configure  <- configureDynamicConstraints(...) + the l/u splice
  *                          reference src/simhelpers.py:11-140, src/trajectorySimulate.py:339-347
  *   mpcqp_cl_step       <- controller select (MPC / LQR failsafe / deadbeat), input-norm clip,
- *                          discrete linear CW plant, perfect-state estimate, termination test
- *                          reference src/trajectorySimulate.py:285-337 (noise=None path)
+ *                          discrete linear CW plant (+ additive noise), perfect-state estimate,
+ *                          range/bearing measurement, termination test
+ *                          reference src/trajectorySimulate.py:285-337
+ *   mpcqp_cl_noise      <- noiseVec = sigMat @ random.normal(0, 1, 4)
+ *                          reference src/trajectorySimulate.py:268,351-356 (counter-based stream
+ *                          per global chaser id instead of numpy's global generator)
+ *   mpcqp_clc_period    <- one sample period of the continuous-time nonlinear loop: controller
+ *                          select at the sample, RK45 plant sub-steps (scipy solve_ivp restated,
+ *                          see mpcqp_estimation.h), measurement, termination test per sub-step
+ *                          reference src/trajectorySimulateC.py:325-409
  *
  * Per-instance arrays are device pointers, row-major [instance][k].  Scenario constants are
  * host values copied into the handle at creation.  Planar model only: nx = 4, nu = 2, ny = 5,
@@ -15,6 +23,8 @@
 #ifndef MPCQP_CLOSED_LOOP_H
 #define MPCQP_CLOSED_LOOP_H
 #include <stdint.h>
+
+#include "mpcqp_estimation.h"
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -46,14 +56,42 @@ int mpcqp_cl_destroy(mpcqp_cl *cl);
  * (reference quirk, src/simhelpers.py:72). */
 int mpcqp_cl_configure(mpcqp_cl *cl, double *xest, double *Ax, double *l, double *u);
 
-/* One control step after a solve.  Inputs: status [B], x_sol [B*n] (u0 read at u0_offset).
+/* One control step after a solve.  Inputs: status [B], x_sol [B*n] (u0 read at u0_offset),
+ * noise [B*4] or NULL (noiseVec added to the plant update).
  * State in/out: x_true [B*4], ctrl_prev [B*2] (the control applied this step: one-sample delay,
- * src/trajectorySimulate.py:323-324), xintf [B], xest [B*6], done [B] (1 once the termination
- * test fired; such instances are frozen), ctrl_seq [B] (1 MPC, 2 failsafe, 3 deadbeat; output),
- * ctrl_out [B*2] (the control chosen this step). */
+ * src/trajectorySimulate.py:323-324), xintf [B], xest [B*6] (set to [x_true, 0, 0]), done [B]
+ * (1 once the termination test fired; such instances are frozen), ctrl_seq [B] (1 MPC,
+ * 2 failsafe, 3 deadbeat, 0 frozen; output), ctrl_out [B*2] (the control chosen this step).
+ * Optional outputs (NULL to skip): z [B*2] the range/bearing measurement of the new true state,
+ * u_applied [B*2] the control the plant applied (the UKF's predict input). */
 int mpcqp_cl_step(mpcqp_cl *cl, const int32_t *status, const double *x_sol, int32_t n,
                   int32_t u0_offset, double *x_true, double *ctrl_prev, double *xintf,
-                  double *xest, int32_t *done, int32_t *ctrl_seq, double *ctrl_out);
+                  double *xest, int32_t *done, int32_t *ctrl_seq, double *ctrl_out,
+                  const double *noise, double *z, double *u_applied);
+
+/* Global id of instance 0 of this handle (a rank's shard offset); keys the noise streams. */
+int mpcqp_cl_set_ids(mpcqp_cl *cl, int64_t id0);
+
+/* noise [B*4] = [sig_x g0, sig_y g1, 0, 0], g ~ N(0, 1) from Philox-4x32-10 with key seed and
+ * counter (draw, global id): draw k of chaser id is the same in every sharding. */
+int mpcqp_cl_noise(mpcqp_cl *cl, uint64_t seed, uint64_t draw, double sig_x, double sig_y,
+                   double *noise);
+
+/* Continuous-time plant of mpcqp_clc_period (isDeltaV: the control is an impulse added to the
+ * velocity at the sample instead of a held acceleration, src/trajectorySimulateC.py:375-380). */
+int mpcqp_cl_set_plant(mpcqp_cl *cl, const mpcqp_plant_model *model, int32_t isDeltaV);
+
+/* One sample period: loop iterations i_start .. i_start + nsub - 1 of trajectorySimulateC, the
+ * first at a sample instant (a solve has just been enqueued).  Arguments as mpcqp_cl_step, plus
+ * iterm [B] (set to the loop index at which the termination test fired), t_start (the
+ * reference's `time` at i_start), dt = T_cont, and traj [B*nsub*4] or NULL (x after every
+ * sub-step).  noise [B*4] is added after every sub-step; z / xest are taken after the first
+ * sub-step, as the reference measures x(i_start + 1). */
+int mpcqp_clc_period(mpcqp_cl *cl, const int32_t *status, const double *x_sol, int32_t n,
+                     int32_t u0_offset, double *x_true, double *ctrl_prev, double *xintf,
+                     double *xest, int32_t *done, int32_t *iterm, int32_t *ctrl_seq,
+                     double *ctrl_out, const double *noise, double *z, double *u_applied,
+                     double t_start, double dt, int32_t i_start, int32_t nsub, double *traj);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,8 @@ EXPORTED = (
     "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
     "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind",
     "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
+    "mpcqp_cl_set_ids", "mpcqp_cl_noise", "mpcqp_cl_set_plant", "mpcqp_clc_period",
+    "mpcqp_ukf_create", "mpcqp_ukf_destroy", "mpcqp_ukf_step", "mpcqp_plant_rk45",
 )
 
 STATUS = {
@@ -76,6 +78,18 @@ class ClScenario(C.Structure):
     ]
 
 
+class UkfModel(C.Structure):
+    _fields_ = [("Ao", C.c_double * 36), ("Bou", C.c_double * 12), ("Q", C.c_double * 36),
+                ("R", C.c_double * 4), ("alpha", C.c_double), ("beta", C.c_double),
+                ("kappa", C.c_double)]
+
+
+class PlantModel(C.Structure):
+    _fields_ = [("two_n", C.c_double), ("m_two_n", C.c_double), ("n2", C.c_double),
+                ("R_T", C.c_double), ("mu", C.c_double), ("g0", C.c_double),
+                ("rtol", C.c_double), ("atol", C.c_double)]
+
+
 _lib = None
 
 
@@ -108,7 +122,17 @@ def lib():
     L.mpcqp_cl_create.argtypes = [C.POINTER(ClScenario), i32, vp, C.POINTER(vp)]
     L.mpcqp_cl_destroy.argtypes = [vp]
     L.mpcqp_cl_configure.argtypes = [vp, dp, dp, dp, dp]
-    L.mpcqp_cl_step.argtypes = [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp]
+    L.mpcqp_cl_step.argtypes = [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]
+    L.mpcqp_cl_set_ids.argtypes = [vp, C.c_int64]
+    L.mpcqp_cl_noise.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_double, C.c_double, dp]
+    L.mpcqp_cl_set_plant.argtypes = [vp, C.POINTER(PlantModel), i32]
+    L.mpcqp_clc_period.argtypes = [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp,
+                                   dp, C.c_double, C.c_double, i32, i32, dp]
+    L.mpcqp_ukf_create.argtypes = [C.POINTER(UkfModel), i32, vp, C.POINTER(vp)]
+    L.mpcqp_ukf_destroy.argtypes = [vp]
+    L.mpcqp_ukf_step.argtypes = [vp, dp, dp, dp, dp, dp, dp]
+    L.mpcqp_plant_rk45.argtypes = [C.POINTER(PlantModel), i32, vp, dp, dp, dp, C.c_double,
+                                   C.c_double, i32, dp, dp]
     L.mpcqp_status_string.argtypes = [i32]
     L.mpcqp_status_string.restype = C.c_char_p
     L.mpcqp_last_error.restype = C.c_char_p

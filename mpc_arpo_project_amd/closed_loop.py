@@ -1,10 +1,16 @@
-"""Batched, device-resident closed loop of the discrete-time linear simulator.
+"""Batched, device-resident closed loops of the reference's simulators.
 
-One `BatchClosedLoop` advances B independent chasers through the reference's control loop
-(reference src/trajectorySimulate.py:285-356, noise=None path) entirely on the GPU:
+`BatchClosedLoop` advances B independent chasers through the discrete-time loop
+(reference src/trajectorySimulate.py:285-356) entirely on the GPU:
 
     solve (HIP engine, warm-started)  ->  controller select + clip + CW plant  (mpcqp_cl_step)
+                                      ->  UKF predict + update (noise != None)  (mpcqp_ukf_step)
                                       ->  configureDynamicConstraints          (mpcqp_cl_configure)
+                                      ->  noise redraw every noise_length steps (mpcqp_cl_noise)
+
+`BatchClosedLoopC` does the same for the continuous-time nonlinear loop
+(src/trajectorySimulateC.py:325-409): one `period()` is a solve at a sample instant followed by
+the RK45 plant sub-steps up to the next sample (mpcqp_clc_period).
 
 The per-step QP data never leaves HBM: the configure kernel rewrites the varying A values and
 bounds in the engine's own buffers.
@@ -62,10 +68,29 @@ def scenario_struct(prob: MPCProblem):
     return sc, keep
 
 
-class BatchClosedLoop:
-    """B chasers of one scenario family stepping through the closed loop on one GPU."""
+def _noise_params(noise):
+    """(sig_x, sig_y, noise_length) from a Noise object or a tuple; None -> None"""
+    if noise is None:
+        return None
+    if hasattr(noise, "noise_std"):
+        return float(noise.noise_std[0]), float(noise.noise_std[1]), noise.noise_length
+    sx, sy, rep = noise
+    return float(sx), float(sy), rep
 
-    def __init__(self, prob: MPCProblem, x0, device="cuda", **settings):
+
+class BatchClosedLoop:
+    """B chasers of one scenario family stepping through the closed loop on one GPU.
+
+    noise: None (the reference's noise=None path: perfect state feedback) or a Noise /
+    (sig_x, sig_y, noise_length): plant noise plus the UKF estimator, as the reference does when
+    noise is not None.  noise_source: None draws noiseVec on the device from a counter-based
+    stream keyed by (noise_seed, global chaser id = id_offset + b, draw index); a callable
+    draw(k) -> (B, 4) array supplies draw k from the host instead (e.g. numpy's seeded global
+    generator, for parity with the reference's own runs).
+    """
+
+    def __init__(self, prob: MPCProblem, x0, device="cuda", noise=None, noise_seed=123,
+                 id_offset=0, noise_source=None, **settings):
         x0 = np.asarray(x0, dtype=float)
         if x0.ndim != 2 or x0.shape[1] != 4:
             raise ValueError("x0 must have shape (B, 4)")
@@ -100,6 +125,45 @@ class BatchClosedLoop:
         self._bufs = data_buffers(self.qp)
         self.u0 = prob.u0_slice.start
         self.steps = 0
+        check(_lib.lib().mpcqp_cl_set_ids(self._cl, int(id_offset)), "mpcqp_cl_set_ids")
+        self._init_noise(noise, noise_seed, noise_source, xest, noise_dt=None)
+
+    def _init_noise(self, noise, seed, source, xest0, noise_dt):
+        self.noise = _noise_params(noise)
+        self.noise_seed, self._noise_source = int(seed), source
+        self.ukf = None
+        self.w = self.z = self.u_applied = None
+        if self.noise is None:
+            return
+        from .estimation import BatchUKF, observer_model
+
+        f = dict(dtype=torch.float64, device=self.device)
+        self.w = torch.zeros(self.B, 4, **f)
+        self.z = torch.zeros(self.B, 2, **f)
+        self.u_applied = torch.zeros(self.B, 2, **f)
+        Ao, Bou, Qw, R, P0 = observer_model(self.prob, self.noise[:2], noise_dt)
+        self.ukf = BatchUKF(Ao, Bou, Qw, R, xest0, P0, device=self.device, stream=self.qp.stream)
+        self._draw(0)
+
+    def _draw(self, k):
+        """noiseVec draw k into self.w (async on the engine stream)"""
+        if self._noise_source is not None:
+            w = np.asarray(self._noise_source(k), dtype=float).reshape(self.B, 4)
+            with torch.cuda.stream(self.qp.stream):
+                self.w.copy_(torch.as_tensor(w), non_blocking=False)
+            return
+        sx, sy = self._noise_scale()
+        check(_lib.lib().mpcqp_cl_noise(self._cl, self.noise_seed, int(k), sx, sy,
+                                        self.w.data_ptr()), "mpcqp_cl_noise")
+
+    def _noise_scale(self):
+        return self.noise[0], self.noise[1]
+
+    def _estimate(self):
+        """UKF step on the measurement the plant kernel produced, estimate -> xest"""
+        self.ukf.step(self.u_applied, self.z, active=self.ctrl_seq)
+        with torch.cuda.stream(self.qp.stream):
+            self.xest.copy_(self.ukf.x)
 
     def step(self):
         """Solve the current QPs, apply the controller and plant, rebuild the QP data (async)."""
@@ -108,17 +172,23 @@ class BatchClosedLoop:
     def step_after_solve(self, r):
         """Controller select + plant + QP-data rebuild for a solve already enqueued (async)."""
         L = _lib.lib()
+        opt = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         rc = L.mpcqp_cl_step(self._cl, r.status.data_ptr(), r.x.data_ptr(), self.qp.n, self.u0,
                              self.x_true.data_ptr(), self.ctrl_prev.data_ptr(),
                              self.xintf.data_ptr(), self.xest.data_ptr(), self.done.data_ptr(),
-                             self.ctrl_seq.data_ptr(), self.ctrl.data_ptr())
+                             self.ctrl_seq.data_ptr(), self.ctrl.data_ptr(), opt(self.w),
+                             opt(self.z), opt(self.u_applied))
         if rc:
             raise MPCQPError(f"mpcqp_cl_step failed ({rc})")
+        if self.ukf is not None:
+            self._estimate()
         ax, l, u = self._bufs
         rc = L.mpcqp_cl_configure(self._cl, self.xest.data_ptr(), ax, l, u)
         if rc:
             raise MPCQPError(f"mpcqp_cl_configure failed ({rc})")
         self.steps += 1
+        if self.noise is not None and self.steps % self.noise[2] == 0:
+            self._draw(self.steps // int(self.noise[2]))
         return r
 
     def close(self):
@@ -126,6 +196,8 @@ class BatchClosedLoop:
             self.qp.stream.synchronize()
             _lib.lib().mpcqp_cl_destroy(self._cl)
             self._cl = None
+        if getattr(self, "ukf", None) is not None:
+            self.ukf.close()
         self.qp.close()
 
     def __del__(self):
@@ -133,3 +205,94 @@ class BatchClosedLoop:
             self.close()
         except Exception:
             pass
+
+
+def sample_schedule(T, T_cont, T_final, i0=500):
+    """The sample periods of trajectorySimulateC's loop (src/trajectorySimulateC.py:323-409):
+    [(i_start, nsub, time at i_start)], the loop index starting at the literal 500, a sample
+    where `disc_j < nsimD and xTimeC[i] == xTimeD[disc_j]`, `time` accumulated by repeated
+    addition of T_cont from T, exactly as the reference does."""
+    nsimD = int(T_final / T)
+    nsimC = int(T_final / T_cont)
+    xTimeD = np.arange(0, T_final, T)
+    xTimeC = np.arange(0, T_final, T_cont)
+    out = []
+    disc_j, time = 1, T
+    for i in range(i0, nsimC - 1):
+        if disc_j < nsimD and xTimeC[i] == xTimeD[disc_j]:
+            out.append([i, 0, time])
+            disc_j += 1
+        elif not out:
+            raise MPCQPError("the first loop iteration of trajectorySimulateC must be a sample")
+        out[-1][1] += 1
+        time = time + T_cont
+    return [tuple(p) for p in out]
+
+
+class BatchClosedLoopC(BatchClosedLoop):
+    """B chasers through the continuous-time nonlinear loop of trajectorySimulateC on one GPU.
+
+    `period()` = the solve at a sample instant + the RK45 plant sub-steps up to the next sample
+    (+ UKF and QP rebuild when noise is given).  `iterm` holds the loop index at which a chaser's
+    termination test fired (nsimC if it never did).  The continuous-time noise of the reference
+    (python-control white_noise with covariance Qcont / 0.001, held for noise_length samples) is
+    drawn from the device stream with that covariance; python-control is absent here, so its exact
+    draws are not reproduced.
+    """
+
+    def __init__(self, prob: MPCProblem, x0, T_cont, T_final, mean_motion, isDeltaV=False,
+                 device="cuda", noise=None, noise_seed=123, id_offset=0, noise_source=None,
+                 **settings):
+        super().__init__(prob, x0, device=device, noise=None, **settings)
+        from .estimation import plant_model
+
+        self.T_cont, self.T_final = float(T_cont), float(T_final)
+        self.schedule = sample_schedule(prob.T, self.T_cont, self.T_final)
+        self.nsimC = int(self.T_final / self.T_cont)
+        self._plant = plant_model(mean_motion)
+        check(_lib.lib().mpcqp_cl_set_plant(self._cl, C.byref(self._plant), int(bool(isDeltaV))),
+              "mpcqp_cl_set_plant")
+        check(_lib.lib().mpcqp_cl_set_ids(self._cl, int(id_offset)), "mpcqp_cl_set_ids")
+        self.iterm = torch.full((self.B,), self.nsimC, dtype=torch.int32, device=self.device)
+        xest = self.xest.cpu().numpy()
+        if prob.inTrack:
+            xest[:, [0, 1]] = xest[:, [1, 0]]
+        hold = int(prob.T / self.T_cont)
+        self._init_noise(noise, noise_seed, noise_source, xest, noise_dt=prob.T * hold)
+        self.period_index = 0
+
+    def _noise_scale(self):
+        s = 1.0 / np.sqrt(0.001)
+        return self.noise[0] * s, self.noise[0] * s  # Qcont = diag(sig_x^2, sig_x^2) (quirk)
+
+    @property
+    def periods(self):
+        return len(self.schedule)
+
+    def period(self, traj=None):
+        """One sample period for every chaser (async); traj: optional (B, nsub, 4) tensor"""
+        if self.period_index >= len(self.schedule):
+            raise MPCQPError("the simulation horizon is exhausted")
+        i0, nsub, t0 = self.schedule[self.period_index]
+        r = self.qp.solve_async()
+        L = _lib.lib()
+        opt = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        if traj is not None and (tuple(traj.shape) != (self.B, nsub, 4) or
+                                 traj.dtype != torch.float64 or not traj.is_contiguous()):
+            raise ValueError("traj must be a contiguous (B, nsub, 4) float64 tensor")
+        check(L.mpcqp_clc_period(self._cl, r.status.data_ptr(), r.x.data_ptr(), self.qp.n,
+                                 self.u0, self.x_true.data_ptr(), self.ctrl_prev.data_ptr(),
+                                 self.xintf.data_ptr(), self.xest.data_ptr(),
+                                 self.done.data_ptr(), self.iterm.data_ptr(),
+                                 self.ctrl_seq.data_ptr(), self.ctrl.data_ptr(), opt(self.w),
+                                 opt(self.z), opt(self.u_applied), t0, self.T_cont, i0, nsub,
+                                 opt(traj)), "mpcqp_clc_period")
+        if self.ukf is not None:
+            self._estimate()
+        ax, l, u = self._bufs
+        check(L.mpcqp_cl_configure(self._cl, self.xest.data_ptr(), ax, l, u),
+              "mpcqp_cl_configure")
+        self.period_index += 1
+        if self.noise is not None and self.period_index % int(self.noise[2]) == 0:
+            self._draw(self.period_index // int(self.noise[2]))
+        return r

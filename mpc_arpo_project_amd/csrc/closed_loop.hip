@@ -12,8 +12,13 @@
 #include <string>
 
 #include "../../include/mpcqp_closed_loop.h"
+#include "../../include/mpcqp_estimation.h"
+#include "plant_dev.hpp"
 
 namespace {
+
+using mpcqp::PlantConsts;
+using mpcqp::rk45_interval;
 
 constexpr int NX = 4, NU = 2, NY = 5, NDI = 2;
 
@@ -89,28 +94,18 @@ __global__ void __launch_bounds__(256) cl_configure_kernel(ClDev d, double* xest
   }
 }
 
-// reference src/trajectorySimulate.py:288-337 for one chaser (noise = None)
-__global__ void __launch_bounds__(256) cl_step_kernel(ClDev d, const int32_t* status,
-                                                      const double* x_sol, int n, int u0,
-                                                      double* x_true, double* ctrl_prev,
-                                                      double* xintf, double* xest, int32_t* done,
-                                                      int32_t* ctrl_seq, double* ctrl_out) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= d.B) return;
-  const mpcqp_cl_scenario& s = d.sc;
-  if (done[b]) {
-    ctrl_seq[b] = 0;
-    return;
-  }
-  const double* xe = xest + (size_t)b * 6;
-  double c0, c1;
+// controller select + input-norm clip (reference src/trajectorySimulate.py:296-319,
+// src/trajectorySimulateC.py:338-361): MPC if the solve succeeded, else deadbeat debris avoidance
+// inside the debris box, else the LQR failsafe; returns the controller id (1 / 3 / 2)
+__device__ __forceinline__ int select_control(const mpcqp_cl_scenario& s, int32_t st,
+                                              const double* xsol, const double* xe, double& xi,
+                                              double& c0, double& c1) {
   int seq;
-  if (status[b] != 1) {
+  if (st != 1) {
     const double h = s.side / 2;
     const bool in_box = s.has_debris && sub(xe[0], add(s.center[0], h)) < 0 &&
                         sub(xe[0], sub(s.center[0], h)) > 0 && xe[1] < add(s.center[1], h) &&
                         xe[1] > sub(s.center[1], h);
-    double xi = xintf[b];
     if (in_box) {  // deadbeat debris avoidance
       double cy = 0.0;
       for (int k = 0; k < NX; ++k) cy = add(cy, mul(s.Crefy[k], xe[k]));
@@ -134,11 +129,10 @@ __global__ void __launch_bounds__(256) cl_step_kernel(ClDev d, const int32_t* st
                mul(s.Kif[1], xi));
       seq = 2;
     }
-    xintf[b] = xi;
   } else {
-    xintf[b] = 0.0;
-    c0 = x_sol[(size_t)b * n + u0];
-    c1 = x_sol[(size_t)b * n + u0 + 1];
+    xi = 0.0;
+    c0 = xsol[0];
+    c1 = xsol[1];
     seq = 1;
   }
   // input-norm clip with the reference's sequential rescale (quirk Q2)
@@ -149,10 +143,48 @@ __global__ void __launch_bounds__(256) cl_step_kernel(ClDev d, const int32_t* st
     nr = sqrt(add(mul(c0, c0), mul(c1, c1)));
     c1 = mul(c1, um / nr);
   }
+  return seq;
+}
+
+// termination test at the top of a loop iteration (src/trajectorySimulate.py:288-293,
+// src/trajectorySimulateC.py:328-333)
+__device__ __forceinline__ bool terminated(const mpcqp_cl_scenario& s, const double* x) {
+  const double rn = sqrt(add(mul(x[0], x[0]), mul(x[1], x[1])));
+  const double pos = s.inTrack ? x[1] : x[0];
+  return rn < s.rp || pos < sub(s.rp, s.rtol);
+}
+
+// range / bearing measurement hx (src/trajectorySimulate.py:330-332)
+__device__ __forceinline__ void measure(const double* x, double* z) {
+  z[0] = sqrt(add(mul(x[0], x[0]), mul(x[1], x[1])));
+  z[1] = atan2(x[1], x[0]);
+}
+
+// reference src/trajectorySimulate.py:288-337 for one chaser: controller, plant
+// x+ = Ad x + Bd u_prev + w (one-sample actuation delay, quirk Q1), perfect-state estimate,
+// optional measurement z of x+ and the applied control (the UKF's predict input)
+__global__ void __launch_bounds__(256) cl_step_kernel(ClDev d, const int32_t* status,
+                                                      const double* x_sol, int n, int u0,
+                                                      double* x_true, double* ctrl_prev,
+                                                      double* xintf, double* xest, int32_t* done,
+                                                      int32_t* ctrl_seq, double* ctrl_out,
+                                                      const double* noise, double* z_out,
+                                                      double* u_applied) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= d.B) return;
+  const mpcqp_cl_scenario& s = d.sc;
+  if (done[b]) {
+    ctrl_seq[b] = 0;
+    return;
+  }
+  const double* xe = xest + (size_t)b * 6;
+  double c0, c1, xi = xintf[b];
+  const int seq = select_control(s, status[b], x_sol + (size_t)b * n + u0, xe, xi, c0, c1);
+  xintf[b] = xi;
   ctrl_seq[b] = seq;
   ctrl_out[(size_t)b * 2] = c0;
   ctrl_out[(size_t)b * 2 + 1] = c1;
-  // plant: x+ = Ad x + Bd u_prev (one-sample actuation delay, quirk Q1); CSC column order
+  // plant in CSC column order (scipy sparse mat-vec), then + noise
   double* xt = x_true + (size_t)b * NX;
   double* up = ctrl_prev + (size_t)b * NU;
   double ax[NX] = {0, 0, 0, 0}, bu[NX] = {0, 0, 0, 0};
@@ -163,18 +195,136 @@ __global__ void __launch_bounds__(256) cl_step_kernel(ClDev d, const int32_t* st
     for (int i = 0; i < NX; ++i)
       if (s.Bd[i * NU + j] != 0.0) bu[i] = add(bu[i], mul(s.Bd[i * NU + j], up[j]));
   double xn[NX];
-  for (int i = 0; i < NX; ++i) xn[i] = add(add(ax[i], bu[i]), 0.0);
+  for (int i = 0; i < NX; ++i)
+    xn[i] = add(add(ax[i], bu[i]), noise ? noise[(size_t)b * NX + i] : 0.0);
   for (int i = 0; i < NX; ++i) xt[i] = xn[i];
+  if (u_applied) {
+    u_applied[(size_t)b * 2] = up[0];
+    u_applied[(size_t)b * 2 + 1] = up[1];
+  }
   up[0] = c0;
   up[1] = c1;
   double* xw = xest + (size_t)b * 6;
   for (int i = 0; i < NX; ++i) xw[i] = xn[i];
   xw[4] = 0.0;
   xw[5] = 0.0;
-  // termination test of the next loop iteration (src/trajectorySimulate.py:288-293)
-  const double rn = sqrt(add(mul(xn[0], xn[0]), mul(xn[1], xn[1])));
-  const double pos = s.inTrack ? xn[1] : xn[0];
-  if (rn < s.rp || pos < sub(s.rp, s.rtol)) done[b] = 1;
+  if (z_out) measure(xn, z_out + (size_t)b * 2);
+  if (terminated(s, xn)) done[b] = 1;
+}
+
+// Philox-4x32-10 (Salmon et al., SC'11): counter (draw, id) under key (seed)
+__device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// noiseVec = sigMat @ normal(0, 1, 4), sigMat = diag(sig_x, sig_y, 0, 0)
+// (src/trajectorySimulate.py:268,352-353), from a counter-based stream keyed by the global chaser
+// id, so that a chaser's noise does not depend on how the batch is sharded
+__global__ void __launch_bounds__(256) cl_noise_kernel(int B, uint64_t seed, int64_t id0,
+                                                       uint64_t draw, double sx, double sy,
+                                                       double* noise) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t id = (uint64_t)(id0 + b);
+  uint32_t c[4] = {(uint32_t)draw, (uint32_t)(draw >> 32), (uint32_t)id, (uint32_t)(id >> 32)};
+  philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  double g[4];
+  for (int k = 0; k < 2; ++k) {  // Box-Muller on (0, 1] uniforms
+    const double u1 = ((double)c[2 * k] + 1.0) * 2.3283064365386963e-10;
+    const double u2 = (double)c[2 * k + 1] * 2.3283064365386963e-10;
+    const double r = sqrt(-2.0 * log(u1));
+    g[2 * k] = r * cos(6.283185307179586 * u2);
+    g[2 * k + 1] = r * sin(6.283185307179586 * u2);
+  }
+  double* o = noise + (size_t)b * NX;
+  o[0] = sx * g[0];
+  o[1] = sy * g[1];
+  o[2] = 0.0;
+  o[3] = 0.0;
+}
+
+// One sample period of the continuous-time closed loop (reference
+// src/trajectorySimulateC.py:325-409) for one chaser: the loop iterations i_s .. i_s + nsub - 1
+// that start at a sample instant i_s.  At i_s: controller select from the estimate of the previous
+// sample; the plant sub-step i_s still runs with the previous control ctrls[:, i_s] (one-sub-step
+// delay); the measurement is taken of x(i_s + 1).  Sub-steps i_s + 1 .. use the new control.
+// Each sub-step: termination test of x(i) (-> done, iterm = i), then
+// x(i+1) = solve_ivp(stateEqnN, (t, t + T_cont), x(i), args=(u,)).y[:, -1] (+ [0, 0, u_prev] at
+// the sample for the delta-v model) + w;  t <- t + T_cont.
+__global__ void __launch_bounds__(64) clc_period_kernel(
+    ClDev d, PlantConsts pc, int isDeltaV, const int32_t* status, const double* x_sol, int n,
+    int u0, double* x_true, double* ctrl_prev, double* xintf, double* xest, int32_t* done,
+    int32_t* iterm, int32_t* ctrl_seq, double* ctrl_out, const double* noise, double* z_out,
+    double* u_applied, double t_start, double dt, int i_start, int nsub, double* traj) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= d.B) return;
+  const mpcqp_cl_scenario& s = d.sc;
+  if (done[b]) {
+    ctrl_seq[b] = 0;
+    return;
+  }
+  const double* xe = xest + (size_t)b * 6;
+  double c0, c1, xi = xintf[b];
+  const int seq = select_control(s, status[b], x_sol + (size_t)b * n + u0, xe, xi, c0, c1);
+  xintf[b] = xi;
+  ctrl_seq[b] = seq;
+  ctrl_out[(size_t)b * 2] = c0;
+  ctrl_out[(size_t)b * 2 + 1] = c1;
+  double* up = ctrl_prev + (size_t)b * NU;
+  const double p0 = up[0], p1 = up[1];
+  if (u_applied) {
+    u_applied[(size_t)b * 2] = p0;
+    u_applied[(size_t)b * 2 + 1] = p1;
+  }
+  double w[NX] = {0, 0, 0, 0};
+  if (noise)
+    for (int i = 0; i < NX; ++i) w[i] = noise[(size_t)b * NX + i];
+  double x[NX];
+  for (int i = 0; i < NX; ++i) x[i] = x_true[(size_t)b * NX + i];
+  double t = t_start;
+  int stop = -1;
+  for (int k = 0; k < nsub; ++k) {
+    if (k > 0 && terminated(s, x)) {
+      stop = i_start + k;
+      break;
+    }
+    const double t1 = add(t, dt);
+    const double ua = isDeltaV ? 0.0 : (k == 0 ? p0 : c0);
+    const double ub = isDeltaV ? 0.0 : (k == 0 ? p1 : c1);
+    rk45_interval(pc, t, t1, x, ua, ub);
+    if (isDeltaV && k == 0) {
+      x[2] = add(x[2], p0);
+      x[3] = add(x[3], p1);
+    }
+    for (int i = 0; i < NX; ++i) x[i] = add(x[i], w[i]);
+    if (traj)
+      for (int i = 0; i < NX; ++i) traj[((size_t)b * nsub + k) * NX + i] = x[i];
+    if (k == 0) {
+      double* xw = xest + (size_t)b * 6;
+      for (int i = 0; i < NX; ++i) xw[i] = x[i];
+      xw[4] = 0.0;
+      xw[5] = 0.0;
+      if (z_out) measure(x, z_out + (size_t)b * 2);
+    }
+    t = t1;
+  }
+  if (stop < 0 && terminated(s, x)) stop = i_start + nsub;
+  if (stop >= 0) {
+    done[b] = 1;
+    iterm[b] = stop;
+  }
+  for (int i = 0; i < NX; ++i) x_true[(size_t)b * NX + i] = x[i];
+  up[0] = c0;
+  up[1] = c1;
 }
 
 thread_local std::string g_cl_err;
@@ -185,6 +335,10 @@ struct mpcqp_cl {
   ClDev d;
   int32_t* dpos = nullptr;
   hipStream_t stream = nullptr;
+  int64_t id0 = 0;          // global id of instance 0 (noise streams)
+  bool has_plant = false;   // continuous-time plant set (mpcqp_cl_set_plant)
+  PlantConsts pc{};
+  int isDeltaV = 0;
 };
 
 extern "C" {
@@ -235,14 +389,54 @@ int mpcqp_cl_configure(mpcqp_cl* cl, double* xest, double* Ax, double* l, double
 
 int mpcqp_cl_step(mpcqp_cl* cl, const int32_t* status, const double* x_sol, int32_t n,
                   int32_t u0_offset, double* x_true, double* ctrl_prev, double* xintf,
-                  double* xest, int32_t* done, int32_t* ctrl_seq, double* ctrl_out) {
+                  double* xest, int32_t* done, int32_t* ctrl_seq, double* ctrl_out,
+                  const double* noise, double* z, double* u_applied) {
   if (!cl || !status || !x_sol || !x_true || !ctrl_prev || !xintf || !xest || !done ||
       !ctrl_seq || !ctrl_out)
     return -1;
   const int B = cl->d.B;
   hipLaunchKernelGGL(cl_step_kernel, dim3((B + 255) / 256), dim3(256), 0, cl->stream, cl->d,
                      status, x_sol, n, u0_offset, x_true, ctrl_prev, xintf, xest, done, ctrl_seq,
-                     ctrl_out);
+                     ctrl_out, noise, z, u_applied);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int mpcqp_cl_set_ids(mpcqp_cl* cl, int64_t id0) {
+  if (!cl || id0 < 0) return -1;
+  cl->id0 = id0;
+  return 0;
+}
+
+int mpcqp_cl_noise(mpcqp_cl* cl, uint64_t seed, uint64_t draw, double sig_x, double sig_y,
+                   double* noise) {
+  if (!cl || !noise) return -1;
+  const int B = cl->d.B;
+  hipLaunchKernelGGL(cl_noise_kernel, dim3((B + 255) / 256), dim3(256), 0, cl->stream, B, seed,
+                     cl->id0, draw, sig_x, sig_y, noise);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int mpcqp_cl_set_plant(mpcqp_cl* cl, const mpcqp_plant_model* m, int32_t isDeltaV) {
+  if (!cl || !m) return -1;
+  cl->pc = PlantConsts{m->two_n, m->m_two_n, m->n2, m->R_T, m->mu, m->g0, m->rtol, m->atol};
+  cl->isDeltaV = isDeltaV ? 1 : 0;
+  cl->has_plant = true;
+  return 0;
+}
+
+int mpcqp_clc_period(mpcqp_cl* cl, const int32_t* status, const double* x_sol, int32_t n,
+                     int32_t u0_offset, double* x_true, double* ctrl_prev, double* xintf,
+                     double* xest, int32_t* done, int32_t* iterm, int32_t* ctrl_seq,
+                     double* ctrl_out, const double* noise, double* z, double* u_applied,
+                     double t_start, double dt, int32_t i_start, int32_t nsub, double* traj) {
+  if (!cl || !cl->has_plant || !status || !x_sol || !x_true || !ctrl_prev || !xintf || !xest ||
+      !done || !iterm || !ctrl_seq || !ctrl_out || nsub < 1 || !(dt > 0.0))
+    return -1;
+  const int B = cl->d.B;
+  hipLaunchKernelGGL(clc_period_kernel, dim3((B + 63) / 64), dim3(64), 0, cl->stream, cl->d,
+                     cl->pc, cl->isDeltaV, status, x_sol, n, u0_offset, x_true, ctrl_prev, xintf,
+                     xest, done, iterm, ctrl_seq, ctrl_out, noise, z, u_applied, t_start, dt,
+                     i_start, nsub, traj);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -22,6 +22,7 @@ def build(extra=()):
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
            "-DMPCQP_TIMING", *extra, os.path.join(csrc, "engine.hip"), os.path.join(csrc, "dense.hip"),
            os.path.join(csrc, "dense_plan.cpp"), os.path.join(csrc, "closed_loop.hip"),
+           os.path.join(csrc, "estimation.hip"),
            os.path.join(csrc, "symbolic.cpp"), "-o", LIB]
     subprocess.check_call(cmd)
 
