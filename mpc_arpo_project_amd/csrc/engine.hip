@@ -59,6 +59,9 @@ struct DevPlan {
   const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
   int n, m, nk, nnzP, nnzA, nnzL;
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
+  // scaling index overlay (symbolic.hpp): 16-byte chunks copied to LDS at u16 offset SCI
+  const uint4* sci_src;
+  int SCI, S_ZERO, sci_n16, sci_eP, sci_eAt, sci_eA, sci_Pi, sci_Pc, sci_Ai, sci_Ac;
 };
 
 struct KParams {
@@ -75,11 +78,15 @@ struct KParams {
   double* scratch;  // [grid][nnzP + nnzA] scaled P and A values of the wave's current instance
   unsigned int* counter;
   unsigned long long* timing;  // diagnostic builds only (MPCQP_TIMING): cycles per phase
+  // initial rho of a cold instance, min(max(settings.rho, RHO_MIN), RHO_MAX), computed on the host:
+  // read per instance from the kernel arguments instead of a loop-invariant register (the gfx950
+  // backend of ROCm 7.2 was seen to spill such a hoisted double and reload only its low half)
+  double rho0;
 };
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
 // s_memtime deltas accumulated per wave in SGPRs, added to p.timing at the end of each instance.
-enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_NSLOT };
+enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_NSLOT };
 #ifdef MPCQP_TIMING
 #define T_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define T_END(slot, v) tacc[slot] += __builtin_amdgcn_s_memtime() - (v)
@@ -450,11 +457,100 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const
       if (o == lane + 64 * r) out[r] = s;
   }
 }
+// out[r] = max_k |v[src]| over the ELL terms of slot r (the infinity norms of Ruiz scaling; max is
+// order-free, so any traversal equals OSQP's).  All index loads are issued before the LDS reads.
+template <int R, int KMAX>
+__device__ __forceinline__ void ell_absmax(const EllDev& e, const uint16_t* src, const double* v,
+                                           double (&out)[R], int lane) {
+  uint32_t ix[R][KMAX];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (e.K[r] == 0) continue;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) ix[r][k] = src[e.off[r] + 64 * k + lane];
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    double mx = 0.0;
+    if (e.K[r] != 0) {
+      double b[KMAX];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) b[k] = v[ix[r][k]];  // padding -> S_ZERO
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) mx = dmaxd(fabs(b[k]), mx);
+    }
+    out[r] = mx;
+  }
+  for (int L = 0; L < e.nlong; ++L) {
+    double mx = 0.0;
+    for (int t = lane; t < e.long_cnt[L]; t += 64) mx = dmaxd(fabs(v[src[e.long_off[L] + t]]), mx);
+    mx = wave_max(mx);
+    const int o = e.long_out[L];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (o == lane + 64 * r) out[r] = mx;
+  }
+}
+// v[base + k] = (v[base + k] * v[oa + ia[k]]) * v[ob + ib[k]] for k < cnt (Ruiz rescale of the
+// matrix values), 8 elements per lane in flight
+__device__ __forceinline__ void scale_vals(double* v, int base, int cnt, const uint16_t* ia,
+                                           const uint16_t* ib, int oa, int ob, int lane) {
+  constexpr int U = 8;
+  for (int k0 = 0; k0 < cnt; k0 += 64 * U) {
+    uint32_t a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane, kc = k < cnt ? k : 0;
+      a[u] = ia[kc];
+      b[u] = ib[kc];
+    }
+    double x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane, kc = k < cnt ? k : 0;
+      x[u] = (v[base + kc] * v[oa + a[u]]) * v[ob + b[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane;
+      if (k < cnt) v[base + k] = x[u];
+    }
+  }
+}
+// v[base + k] = src[k] for k < cnt, 8 loads per lane in flight
+__device__ __forceinline__ void load_vals(double* v, int base, const double* src, int cnt,
+                                          int lane) {
+  constexpr int U = 8;
+  for (int k0 = 0; k0 < cnt; k0 += 64 * U) {
+    double x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane;
+      x[u] = src[k < cnt ? k : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane;
+      if (k < cnt) v[base + k] = x[u];
+    }
+  }
+}
 // gather the scaled values (scaling overlay in LDS) into the slab's ELL copies
-__device__ __forceinline__ void ell_park(const EllDev& e, double* dst, const double* v, int lane) {
-  for (int t = lane; t < e.total; t += 64) {
-    const uint32_t src = e.src[t];
-    dst[t] = src != 0xffffu ? v[src] : 0.0;
+__device__ __forceinline__ void ell_park(const EllDev& e, const uint16_t* src, double* dst,
+                                         const double* v, int lane) {
+  constexpr int U = 8;
+  for (int t0 = 0; t0 < e.total; t0 += 64 * U) {
+    double x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + 64 * u + lane;
+      x[u] = v[src[t < e.total ? t : 0]];  // padding -> S_ZERO
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + 64 * u + lane;
+      if (t < e.total) dst[t] = x[u];
+    }
   }
 }
 
@@ -751,20 +847,41 @@ __device__ __forceinline__ bool has_solution(int st) {
          st != MPCQP_NON_CVX;
 }
 
-// Ruiz equilibration (scaling.c scale_data) of the instance's P (shared values) and A, q, l, u.
-// Leaves scaled P/A in the slab, D, 1/D, E, 1/E in the slab, and q, l, u (scaled) and the
-// constraint classes in registers.
+// Ruiz equilibration (scaling.c scale_data) of the instance's P (shared values) and A, q, l, u:
+// the passes.  Matrix values live in the LDS scaling overlay (S_P, S_A, D_temp, E_temp); the index
+// lists the passes walk are copied into LDS once (the scaling index overlay, symbolic.hpp), so a
+// pass is LDS traffic only.  The column / row norms use the padded ELL lists (max is order-free);
+// padding entries read the zero slot S_ZERO, so no LDS read is conditional.  Returns D and E;
+// q, l, u (scaled) and c are left in S.
 template <int RN, int RM>
-__device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs, Inst<RN, RM>& S, const Slab& sb,
-                              double* v, int lane) {
+__device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<RN, RM>& S,
+                                              double* v, int lane, double (&D)[RN], double (&E)[RM]) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
   const double* Ax_in = p.Ax + (size_t)inst * P.nnzA;
   const double* l_in = p.l + (size_t)inst * m;
   const double* u_in = p.u + (size_t)inst * m;
-  double D[RN], E[RM];
-  for (int k = lane; k < P.nnzP; k += 64) v[P.S_P + k] = p.Px[k];
-  for (int k = lane; k < P.nnzA; k += 64) v[P.S_A + k] = Ax_in[k];
+  {  // scaling index overlay -> LDS (read by every pass below and by scale_finish)
+    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(v) + P.SCI);
+    constexpr int U = 8;
+    for (int k0 = 0; k0 < P.sci_n16; k0 += 64 * U) {
+      uint4 t[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + 64 * u + lane;
+        t[u] = P.sci_src[k < P.sci_n16 ? k : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + 64 * u + lane;
+        if (k < P.sci_n16) d[k] = t[u];
+      }
+    }
+  }
+  if (lane == 0) v[P.S_ZERO] = 0.0;
+  const uint16_t* ix = reinterpret_cast<const uint16_t*>(v) + P.SCI;
+  load_vals(v, P.S_P, p.Px, P.nnzP, lane);
+  load_vals(v, P.S_A, Ax_in, P.nnzA, lane);
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
@@ -781,36 +898,28 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
   S.c = 1.0;
   LDS_FENCE();
   for (int it = 0; it < p.s.scaling; ++it) {
-    double dt[RN], et[RM];
+    // compute_inf_norm_cols_KKT: columns of [P A'; A 0] (P symmetric from its upper triangle)
+    double dp[RN], da[RN], er[RM], dt[RN], et[RM];
+    ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dp, lane);
+    ell_absmax<RN, ELL_KAT>(P.eAt, ix + P.sci_eAt, v, da, lane);
+    ell_absmax<RM, ELL_KA>(P.eA, ix + P.sci_eA, v, er, lane);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const int j = lane + 64 * r;
-      double d = 0.0;
-      if (j < n) {
-        for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) d = dmaxd(fabs(v[P.S_P + P.Psk[e]]), d);
-        double da = 0.0;
-        for (int k = P.Ap[j]; k < P.Ap[j + 1]; ++k) da = dmaxd(fabs(v[P.S_A + k]), da);
-        d = dmaxd(d, da);
-      }
-      d = sqrt(limit_scaling(d));
-      dt[r] = 1. / d;
+      const double d = j < n ? dmaxd(dp[r], da[r]) : 0.0;
+      dt[r] = 1. / sqrt(limit_scaling(d));
       if (j < n) v[P.S_DT + j] = dt[r];
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       const int i = lane + 64 * r;
-      double e = 0.0;
-      if (i < m)
-        for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) e = dmaxd(fabs(v[P.S_A + P.Ark[q]]), e);
-      e = sqrt(limit_scaling(e));
-      et[r] = 1. / e;
+      const double e = i < m ? er[r] : 0.0;
+      et[r] = 1. / sqrt(limit_scaling(e));
       if (i < m) v[P.S_ET + i] = et[r];
     }
     LDS_FENCE();
-    for (int k = lane; k < P.nnzP; k += 64)
-      v[P.S_P + k] = (v[P.S_P + k] * v[P.S_DT + P.Pi[k]]) * v[P.S_DT + P.Pcol[k]];
-    for (int k = lane; k < P.nnzA; k += 64)
-      v[P.S_A + k] = (v[P.S_A + k] * v[P.S_ET + P.Ai[k]]) * v[P.S_DT + P.Acol[k]];
+    scale_vals(v, P.S_P, P.nnzP, ix + P.sci_Pi, ix + P.sci_Pc, P.S_DT, P.S_DT, lane);
+    scale_vals(v, P.S_A, P.nnzA, ix + P.sci_Ai, ix + P.sci_Ac, P.S_ET, P.S_DT, lane);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       S.q[r] = dt[r] * S.q[r];
@@ -819,15 +928,14 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
 #pragma unroll
     for (int r = 0; r < RM; ++r) E[r] = E[r] * et[r];
     LDS_FENCE();
-    // cost normalization
+    // cost normalization: mean of P's column norms, |q|_inf
+    ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dp, lane);
     double csum = 0.0, qmax = 0.0;
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const int j = lane + 64 * r;
       if (j < n) {
-        double d = 0.0;
-        for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) d = dmaxd(fabs(v[P.S_P + P.Psk[e]]), d);
-        csum += d;
+        csum += dp[r];
         qmax = dmaxd(qmax, fabs(S.q[r]));
       }
     }
@@ -841,6 +949,16 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
     S.c = S.c * c_temp;
     LDS_FENCE();
   }
+}
+
+// end of scale_data: constraint classes, scaled bounds, D / E and the scaled matrices parked in
+// the per-wave slab (and their ELL copies for the residual mat-vecs)
+template <int RN, int RM>
+__device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs, Inst<RN, RM>& S,
+                                             const Slab& sb, double* v, int lane, const double (&D)[RN],
+                                             const double (&E)[RM]) {
+  const DevPlan& P = p.pl;
+  const int n = P.n, m = P.m;
   S.cinv = 1. / S.c;
   // constraint classes (auxil.c set_rho_vec / update_rho_vec): with warm state OSQP classifies
   // on bounds scaled by the PREVIOUS equilibration (update_bounds precedes the rescale of
@@ -873,9 +991,10 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
   // park scaled P, A for residuals / refactorization (per-wave slab)
   for (int k = lane; k < P.nnzP; k += 64) sb.Ps[k] = v[P.S_P + k];
   for (int k = lane; k < P.nnzA; k += 64) sb.As[k] = v[P.S_A + k];
-  ell_park(P.eA, sb.vA, v, lane);
-  ell_park(P.eAt, sb.vAt, v, lane);
-  ell_park(P.eP, sb.vP, v, lane);
+  const uint16_t* ix = reinterpret_cast<const uint16_t*>(v) + P.SCI;
+  ell_park(P.eA, ix + P.sci_eA, sb.vA, v, lane);
+  ell_park(P.eAt, ix + P.sci_eAt, sb.vAt, v, lane);
+  ell_park(P.eP, ix + P.sci_eP, sb.vP, v, lane);
   LDS_FENCE();
 }
 
@@ -891,9 +1010,15 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   unsigned long long tacc[T_NSLOT] = {};
 #endif
   T_BEGIN(t_sc);
-  scale_problem<RN, RM>(p, inst, hs, S, sb, v, lane);
+  {
+    double D[RN], E[RM];
+    scale_problem<RN, RM>(p, inst, S, v, lane, D, E);
+    T_BEGIN(t_sf);
+    scale_finish<RN, RM>(p, inst, hs, S, sb, v, lane, D, E);
+    T_END(T_SCFIN, t_sf);
+  }
   T_END(T_SCALE, t_sc);
-  S.rho = (hs != 0) ? p.rho_state[inst] : dmind(dmaxd(p.s.rho, RHO_MIN), RHO_MAX);
+  S.rho = (hs != 0) ? p.rho_state[inst] : p.rho0;
   set_rho(S);
   T_BEGIN(t_f0);
   assemble_and_factor<RN, RM>(p, sb, v, lane, S);
@@ -1357,7 +1482,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
            o_Pso = push_blob(blob, pl.Pso), o_eAs = push_blob(blob, pl.ellA.src),
            o_eAi = push_blob(blob, pl.ellA.in), o_eTs = push_blob(blob, pl.ellAt.src),
            o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
-           o_ePi = push_blob(blob, pl.ellP.in);
+           o_ePi = push_blob(blob, pl.ellP.in), o_sci = push_blob(blob, pl.sci_block);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
@@ -1393,6 +1518,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.CACC = pl.CACC, dp.ZERO = pl.ZERO;
     dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N;
     dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
+    dp.sci_src = (const uint4*)(b + o_sci), dp.SCI = pl.SCI, dp.S_ZERO = pl.S_ZERO;
+    dp.sci_n16 = (int)(pl.sci_block.size() / 8);
+    dp.sci_eP = pl.sci_eP, dp.sci_eAt = pl.sci_eAt, dp.sci_eA = pl.sci_eA;
+    dp.sci_Pi = pl.sci_Pi, dp.sci_Pc = pl.sci_Pc, dp.sci_Ai = pl.sci_Ai, dp.sci_Ac = pl.sci_Ac;
 
     // occupancy (LDS image and VGPRs) -> persistent grid
     int dev = 0, ncu = 0;
@@ -1518,6 +1647,7 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   p.scratch = h->scratch;
   p.counter = h->counter;
   p.timing = h->timing;
+  p.rho0 = std::min(std::max(h->set.rho, RHO_MIN), RHO_MAX);
   HIPCHK(hipMemsetAsync(h->counter, 0, 64, h->stream));
   if (h->dense) {
     DenseSolveArgs a{};

@@ -789,6 +789,34 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     pl.error = "problem too large for the residual layout";
     return false;
   }
+  // ---- scaling index overlay behind the scaling value overlay (grows the image only if needed)
+  {
+    auto& b = pl.sci_block;
+    b.clear();
+    auto put = [&](const std::vector<uint16_t>& v, int cnt, int& off) {
+      off = (int)b.size();
+      b.insert(b.end(), v.begin(), v.begin() + cnt);
+    };
+    put(pl.ellP.src, pl.ellP.total, pl.sci_eP);
+    put(pl.ellAt.src, pl.ellAt.total, pl.sci_eAt);
+    put(pl.ellA.src, pl.ellA.total, pl.sci_eA);
+    put(pl.Pi, pl.nnzP, pl.sci_Pi);
+    put(pl.Pcol, pl.nnzP, pl.sci_Pc);
+    put(pl.Ai, pl.nnzA, pl.sci_Ai);
+    put(pl.Acol, pl.nnzA, pl.sci_Ac);
+    while (b.size() % 8) b.push_back(0);
+    // ELL padding reads a zero double kept behind the value overlay (no conditional LDS reads)
+    pl.S_ZERO = pl.S_ET + m;
+    for (int k = 0; k < pl.sci_Pi; ++k)
+      if (b[k] == 0xffff) b[k] = (uint16_t)pl.S_ZERO;
+    pl.SCI = ((pl.S_ZERO + 1) * 4 + 7) & ~7;  // u16 units, 16-byte aligned
+    const int end = pl.SCI + (int)b.size();
+    if (end > pl.LDS_N * 4) pl.LDS_N = (((end + 3) / 4) + 1) & ~1;
+    if (pl.LDS_N * 8 > (int)META_TGT_MASK || pl.LDS_N >= 65535) {
+      pl.error = "LDS image too large for the scaling index overlay";
+      return false;
+    }
+  }
   return true;
 }
 

@@ -82,6 +82,12 @@ struct Plan {
   int nN = 0, nG = 0, nGP = 0;
   // scaling-phase overlay of the same LDS: scaled P, scaled A, D_temp, E_temp
   int S_P = 0, S_A = 0, S_DT = 0, S_ET = 0;
+  // scaling index overlay (LDS, u16 units from the image base, 16-byte aligned): the ELL src
+  // lists of P, A', A and the (row, column) of every P and A entry, copied in once per solve so
+  // the Ruiz passes read indices from LDS; offsets relative to SCI
+  int SCI = 0, S_ZERO = 0;  // S_ZERO: a zero double (in doubles) for the ELL padding
+  int sci_eP = 0, sci_eAt = 0, sci_eA = 0, sci_Pi = 0, sci_Pc = 0, sci_Ai = 0, sci_Ac = 0;
+  std::vector<uint16_t> sci_block;  // padded to a multiple of 8 entries
   // KKT assembly: LDS slot of each P entry (diagonal -> D slot), A entry, rho diagonal,
   // sigma diagonal (D slot of x_j)
   std::vector<uint16_t> slotP, slotA, slotRho, slotSig;

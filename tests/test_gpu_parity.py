@@ -167,3 +167,28 @@ def test_dense_engine_opt_in(golden, monkeypatch):
     assert np.max(np.abs(xg[ok][:, sl] - xo[ok][:, sl])) < 1e-6
     monkeypatch.delenv("MPCQP_ENGINE")
     assert BatchQP(prob.P, prob.A, batch=4, **st).schedule_info()["engine"] == "kkt"
+
+
+def test_repeated_solves_are_bit_identical(golden):
+    """fresh handles, one instance per launch and re-used handles give bit-identical results (a
+    guard against reads of stale device state; it caught a backend spill miscompile once)"""
+    from conftest import problem
+
+    for Nx, dv, tag in ((20, False, "batch_n20"), (40, True, "batch_n40dv")):
+        prob = problem(Nx, dv)
+        d = golden(tag)
+        st = dict(eps_abs=1e-4, eps_rel=1e-4)
+        runs = []
+        for _ in range(2):
+            qp = BatchQP(prob.P, prob.A, batch=8, **st)
+            qp.set_data(q=prob.q, Ax=d["Ax"][:8], l=d["l"][:8], u=d["u"][:8])
+            r = qp.solve()
+            runs.append((r.status.cpu().numpy(), r.iter.cpu().numpy(), r.x.cpu().numpy()))
+        for b in range(3):
+            qp = BatchQP(prob.P, prob.A, batch=1, **st)
+            qp.set_data(q=prob.q, Ax=d["Ax"][b:b + 1], l=d["l"][b:b + 1], u=d["u"][b:b + 1])
+            r = qp.solve()
+            assert int(r.status[0]) == runs[0][0][b] and int(r.iter[0]) == runs[0][1][b]
+            assert np.array_equal(r.x.cpu().numpy()[0], runs[0][2][b], equal_nan=True)
+        for k in range(3):
+            assert np.array_equal(runs[0][k], runs[1][k], equal_nan=True)

@@ -14,7 +14,8 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.environ.get("MPCQP_TIMING_LIB") or os.path.join(REPO, "tools", "libmpcqp_timing.so")
-SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact", "resid", "term", "nchk", "adapt"]
+SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact", "resid", "term", "nchk", "adapt",
+         "scale_finish"]
 
 
 def build(extra=()):
@@ -81,6 +82,7 @@ def run(B=65536, steps=5, warmup=3, nx=20):
                                 "term": t["term"] / max(t["nchk"], 1),
                                 "adapt": t["adapt"] / max(t["nchk"], 1),
                                 "check_total": t["check"] / max(t["nchk"], 1)},
+           "scale_finish_per_solve": t["scale_finish"] / n_inst,
            "cycles_per_solve_step": {"fwd": t["fwd"] / iters / sched["fwd_steps"],
                                      "bwd": t["bwd"] / iters / sched["bwd_steps"]},
            "cycles_per_factor_step": t["factor"] / max(t["nfact"], 1) / sched["fac_steps"],
