@@ -185,11 +185,10 @@ __device__ __forceinline__ Rsrc table_rsrc(const uint32_t* tbl, int nsteps, int 
                                            nsteps * stride_words * 4, 0x00020000);
 }
 
-// one lane's records of a solve step: 4 segment quads (a0, b0, a1, b1), targets t0..t3, meta
+// one lane's records of a solve step: 4 segment quads (a0, b0, a1, b1), targets t0..t3
 struct SolveRec {
   uint32_t a[SOLVE_MAXC], b[SOLVE_MAXC];
   uint32_t t0, t1, t2, t3;
-  uint32_t mt;
 };
 __device__ __forceinline__ void load_solve(Rsrc rs, int soff, uint32_t lane, SolveRec& r) {
 #pragma unroll
@@ -200,8 +199,6 @@ __device__ __forceinline__ void load_solve(Rsrc rs, int soff, uint32_t lane, Sol
   const auto tg =
       __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + 4 * SOLVE_TERM_WORDS, soff, 0);
   r.t0 = tg[0], r.t1 = tg[1], r.t2 = tg[2], r.t3 = tg[3];
-  r.mt = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lane * 4u) + 4 * SOLVE_TERM_WORDS + 1024,
-                                              soff, 0);
 }
 // one lane's records of a factorization step: meta word + FAC_MAXC (a, b, c, -) address quads
 struct FacRec {
@@ -242,37 +239,31 @@ __device__ __forceinline__ double dot3(const double* v, const FacRec& r) {
   return a0 + a1;
 }
 
-// One solve step.  Negated segment sums n_q = -(v[a_2q] v[b_2q] + v[a_2q+1] v[b_2q+1]) (the FMA
-// negate modifiers are free); output 0 is the lane's whole sum (FULL, then reduced over the lane
-// group), n0 + n1 (H0) or n0; output 2 is n2 + n3 (H1) or n2; outputs 1 and 3 are n1 and n3.
-// Output q is stored to target t_q; unused targets are the lane's sink slot and the lanes of a
-// group store the group's bitwise-identical sum to the same slot, so no store needs a branch.
-// Steps with fewer terms per lane read the ZERO slot in their unused term slots.
+// One solve step: segment sums n_q = -(v[a_2q] v[b_2q] + v[a_2q+1] v[b_2q+1]) (the FMA negate
+// modifiers are free) are added to targets t_q with LDS atomics (ds_add_f64, no return).  A wave's
+// LDS instructions execute in issue order, so the next step's reads see these sums.  Unused
+// segments read the ZERO slot and add 0 to the lane's sink slot, so nothing needs a branch.
+__device__ __forceinline__ void lds_add(uint32_t a, double x) {
+  __hip_atomic_fetch_add((lds_double*)(size_t)a, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(r.mt);
-  const uint32_t glog = (m0 >> META_SGLOG_SHIFT) & 7u;
-  const uint32_t gl = (r.mt >> META_GLOG_SHIFT) & 7u;
   double x[8], y[8];
 #pragma unroll
+#ifdef EXP_NO_LDSREAD  // timing ablation: operands from the record words instead of LDS
+  for (int c = 0; c < 8; ++c) x[c] = (double)r.a[c], y[c] = (double)r.b[c];
+#else
   for (int c = 0; c < 8; ++c) x[c] = lds_ld(v, r.a[c]), y[c] = lds_ld(v, r.b[c]);
+#endif
   __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
   __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
   const double n0 = fma(-x[1], y[1], -(x[0] * y[0]));
   const double n1 = fma(-x[3], y[3], -(x[2] * y[2]));
   const double n2 = fma(-x[5], y[5], -(x[4] * y[4]));
   const double n3 = fma(-x[7], y[7], -(x[6] * y[6]));
-  const double p01 = n0 + n1, p23 = n2 + n3;
-  double o0 = (r.mt & META_FULL) ? p01 + p23 : ((r.mt & META_H0) ? p01 : n0);
-  const double o2 = (r.mt & META_H1) ? p23 : n2;
-#ifndef EXP_NO_LADDER  // timing ablations (tools/phase_timing.py builds only; results wrong)
-  o0 = group_sum(o0, glog, gl);
-#endif
-  lds_st(v, r.t0, o0);
-#ifndef EXP_NO_STORE123
-  lds_st(v, r.t1, n1);
-  lds_st(v, r.t2, o2);
-  lds_st(v, r.t3, n3);
-#endif
+  lds_add(r.t0, n0);
+  lds_add(r.t1, n1);
+  lds_add(r.t2, n2);
+  lds_add(r.t3, n3);
   LDS_FENCE();
 }
 // One factorization step: v[t] <- -sum_c v[a_c] v[b_c] v[c_c]; a D_j target also writes 1/D_j at
@@ -320,12 +311,18 @@ __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops
 // The rotation is unrolled 12 steps deep: LLVM's waitcnt insertion merges states pessimistically
 // at a loop header (the first step after it would wait for all three sets), so the header is
 // reached at most once per ~12 steps.
+#ifdef EXP_NO_RECLOAD  // timing ablation: the three prefetched record sets are reused
+#define MPCQP_STEP(X)                                       \
+  ops.step(p.X);                                            \
+  if (++s >= n) break;
+#else
 #define MPCQP_STEP(X)                                       \
   ops.step(p.X);                                            \
   if (++s >= n) break;                                      \
   __builtin_amdgcn_sched_barrier(0);                        \
   Ops::load(rs, step_off<Ops>(n, s + 2), lane, p.X);        \
   __builtin_amdgcn_sched_barrier(0);
+#endif
 template <typename Ops>
 __device__ __forceinline__ void run_body(Rsrc rs, int n, uint32_t lane, const Ops& ops,
                                          Pipe<Ops>& p) {
@@ -1120,6 +1117,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
       if (i < m) v[wsz[r] + coff] = bz[r];
     }
+    for (int k = lane; k < P.nk; k += 64) v[P.W + k] = 0.0;  // the solve accumulates into W
     LDS_FENCE();
     T_END(T_VEC, t_v0);
     T_BEGIN(t_fw);
@@ -1127,7 +1125,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     T_END(T_FWD, t_fw);
     T_BEGIN(t_v1);
     prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
-    for (int k = lane; k < P.nk; k += 64) v[P.CACC + k] = v[P.W + k] * v[P.DINV + k];
+    for (int k = lane; k < P.nk; k += 64) {
+      v[P.CACC + k] = v[P.W + k] * v[P.DINV + k];
+      v[P.W + k] = 0.0;
+    }
     LDS_FENCE();
     T_END(T_VEC, t_v1);
     T_BEGIN(t_bw);

@@ -141,131 +141,185 @@ int pack_fac_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<u
   return nsteps;
 }
 
-// Pack one solve level into fixed-stride 64-lane steps appended to tbl.  A lane's 8 term slots are
-// 4 two-term segments (quarters): tasks of <= 2 terms take a quarter, <= 4 a half, <= 8 a whole
-// lane, longer ones an aligned group of whole lanes (META_FULL).  Every lane stores all four
-// segment outputs (unused ones to its sink slot), so stores need no branch.
+// Pack one solve level into fixed-stride 64-lane steps appended to tbl.  Solve tasks accumulate:
+// every two-term segment  -(v[a0] v[b0] + v[a1] v[b1])  is added to its target with an LDS atomic
+// (ds_add_f64), so a task's terms may be spread over any segments of any lanes and any number of
+// consecutive steps (the targets start at zero or hold the in-place value; symbolic.hpp).  Unused
+// segments read the ZERO slot and add 0 to the lane's sink slot.
+//
+// The solves are LDS-bound (four waves share a CU's LDS), so segments are placed to minimise LDS
+// bank conflicts (MI355X: ds_read_b64 serves two 32-lane halves, double bank = slot mod 32, equal
+// addresses broadcast; the atomic serves four 16-lane groups, double bank = slot mod 16, equal
+// addresses serialise): each segment goes to the free (lane, segment) position whose vector
+// operands and target collide least with those already placed.  The matrix operands are made
+// conflict-free afterwards by permuting their LDS slots (layout_matrix_values).
 int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<uint32_t>& tbl) {
   if (getenv("MPCQP_DUMP_TASKS")) {
     fprintf(stderr, "level:");
-    for (const Task& t : tasks) fprintf(stderr, " %zu", t.terms.size() + (t.inplace ? 1 : 0));
+    for (const Task& t : tasks) fprintf(stderr, " %zu", t.terms.size());
     fprintf(stderr, "\n");
   }
-  struct Item {
-    const Task* t;
-    int units, g, glog;  // quarters needed (1, 2, 4) or lanes (g) for groups
+  struct Seg {
+    int target;
+    int a0, b0, a1, b1;
   };
+  std::vector<Seg> segs;
+  for (const Task& t : tasks)
+    for (size_t k = 0; k < t.terms.size(); k += 2) {
+      Seg g{t.target, t.terms[k][0], t.terms[k][1], pl.ZERO, pl.ZERO};
+      if (k + 1 < t.terms.size()) g.a1 = t.terms[k + 1][0], g.b1 = t.terms[k + 1][1];
+      segs.push_back(g);
+    }
   const uint32_t zb = (uint32_t)pl.ZERO * 8u;
   int nsteps = 0;
-  for (const auto& rt : make_rounds(tasks, 64 * SOLVE_MAXC, pl)) {
-    std::vector<Item> items;
-    for (const Task& t : rt) {
-      const int nt = (int)t.terms.size();
-      Item it{&t, 0, 1, 0};
-      if (nt <= 2) {
-        it.units = 1;
-      } else if (nt <= 4) {
-        it.units = 2;
-      } else {
-        it.units = 4;
-        while (it.g < 64 && (nt + it.g - 1) / it.g > SOLVE_MAXC) it.g *= 2, it.glog++;
+  for (size_t s0 = 0; s0 < segs.size(); s0 += 256) {
+    const size_t s1 = std::min(segs.size(), s0 + 256);
+    const size_t base = tbl.size();
+    tbl.resize(base + SOLVE_STEP_WORDS, zb);
+    uint32_t* terms = tbl.data() + base;
+    uint32_t* tg = terms + SOLVE_TERM_WORDS;
+    for (int l = 0; l < 64; ++l)
+      for (int q = 0; q < 4; ++q) tg[l * 4 + q] = (uint32_t)(pl.SINK + l) * 8u;
+    // occupancy: vector reads per (term slot c, half, bank) -> addresses; atomics per (q, group,
+    // bank) -> count
+    std::vector<std::vector<int>> rd(8 * 2 * 32);
+    std::vector<int> at(4 * 4 * 16, 0);
+    std::vector<char> used(256, 0);
+    auto rd_pen = [&](int c, int h, int b) {
+      if (b == pl.ZERO) return 0;
+      const auto& v = rd[(c * 2 + h) * 32 + b % 32];
+      for (int x : v)
+        if (x == b) return 0;  // broadcast
+      return (int)v.size();
+    };
+    for (size_t s = s0; s < s1; ++s) {
+      const Seg& g = segs[s];
+      int best = -1, bestp = 1 << 30;
+      for (int pos = 0; pos < 256; ++pos) {
+        if (used[pos]) continue;
+        const int l = pos / 4, q = pos % 4, h = l / 32, grp = l / 16;
+        int pen = 4 * at[(q * 4 + grp) * 16 + g.target % 16];
+        pen += rd_pen(2 * q, h, g.b0) + rd_pen(2 * q + 1, h, g.b1);
+        if (pen < bestp) bestp = pen, best = pos;
+        if (pen == 0) break;
       }
-      items.push_back(it);
+      used[best] = 1;
+      const int l = best / 4, q = best % 4, h = l / 32, grp = l / 16;
+      at[(q * 4 + grp) * 16 + g.target % 16]++;
+      auto add_rd = [&](int c, int b) {
+        if (b == pl.ZERO) return;
+        auto& v = rd[(c * 2 + h) * 32 + b % 32];
+        if (std::find(v.begin(), v.end(), b) == v.end()) v.push_back(b);
+      };
+      add_rd(2 * q, g.b0);
+      add_rd(2 * q + 1, g.b1);
+      uint32_t* w = terms + q * 256 + l * 4;  // segment row q, lane quad (a0, b0, a1, b1)
+      w[0] = (uint32_t)g.a0 * 8u, w[1] = (uint32_t)g.b0 * 8u;
+      w[2] = (uint32_t)g.a1 * 8u, w[3] = (uint32_t)g.b1 * 8u;
+      tg[l * 4 + q] = (uint32_t)g.target * 8u;
     }
-    std::stable_sort(items.begin(), items.end(), [](const Item& x, const Item& y) {
-      if (x.g != y.g) return x.g > y.g;
-      return x.units > y.units;
-    });
-    std::vector<Item> pending = items;
-    while (!pending.empty()) {
-      // per lane: occupied quarters (bit mask), task per quarter
-      uint32_t occ[64] = {};
-      const Task* qt[64][4] = {};
-      uint32_t flags[64] = {};
-      int lglog[64] = {};
-      std::vector<Item> deferred;
-      int C = 0, sglog = 0;
-      for (const Item& it : pending) {
-        bool placed = false;
-        if (it.units == 4) {
-          for (int off = 0; off + it.g <= 64 && !placed; off += it.g) {
-            bool free = true;
-            for (int r = 0; r < it.g; ++r) free = free && occ[off + r] == 0;
-            if (!free) continue;
-            const int nt = (int)it.t->terms.size();
-            for (int r = 0; r < it.g; ++r) {
-              occ[off + r] = 15u;
-              qt[off + r][0] = it.t;
-              flags[off + r] = META_FULL;
-              lglog[off + r] = it.glog;
-            }
-            C = std::max(C, (nt + it.g - 1) / it.g);
-            sglog = std::max(sglog, it.glog);
-            placed = true;
-          }
-        } else {
-          const uint32_t need = it.units == 2 ? 3u : 1u;
-          const int stride = it.units;
-          // first fit, preferring lanes already in use (keeps whole lanes free for later items)
-          for (int pass = 0; pass < 2 && !placed; ++pass)
-            for (int l = 0; l < 64 && !placed; ++l) {
-              if ((pass == 0) != (occ[l] != 0)) continue;
-              for (int q = 0; q < 4 && !placed; q += stride) {
-                if (occ[l] & (need << q)) continue;
-                occ[l] |= need << q;
-                qt[l][q] = it.t;
-                if (it.units == 2) flags[l] |= q == 0 ? META_H0 : META_H1;
-                C = std::max(C, 2 * q + (int)it.t->terms.size());
-                placed = true;
-              }
-            }
-        }
-        if (!placed) deferred.push_back(it);
-      }
-      C = C <= 2 ? 2 : (C <= 4 ? 4 : 8);
-      const size_t base = tbl.size();
-      tbl.resize(base + SOLVE_STEP_WORDS, zb);
-      uint32_t* terms = tbl.data() + base;
-      uint32_t* tg = terms + SOLVE_TERM_WORDS;
-      uint32_t* meta = tg + 64 * 4;
-      // term slot c of lane l: segment row c / 2, word 2 * (c % 2) of the lane's quad
-      auto slot = [&](int c, int l) { return terms + (c / 2) * 256 + l * 4 + (c % 2) * 2; };
-      for (int l = 0; l < 64; ++l) {
-        meta[l] = ((uint32_t)C << META_C_SHIFT) | ((uint32_t)sglog << META_SGLOG_SHIFT) | flags[l] |
-                  ((uint32_t)lglog[l] << META_GLOG_SHIFT);
-        const uint32_t sink = (uint32_t)(pl.SINK + l) * 8u;
-        for (int q = 0; q < 4; ++q) tg[l * 4 + q] = qt[l][q] ? (uint32_t)qt[l][q]->target * 8u : sink;
-      }
-      // terms: group tasks strided over their lanes, others from the first slot of their segment
-      std::vector<const Task*> done;
-      for (int l = 0; l < 64; ++l)
-        for (int q = 0; q < 4; ++q) {
-          const Task* t = qt[l][q];
-          if (!t) continue;
-          if (flags[l] & META_FULL) {
-            if (std::find(done.begin(), done.end(), t) != done.end()) continue;
-            done.push_back(t);
-            int g = 0;  // lanes of the group (consecutive, starting here)
-            while (l + g < 64 && qt[l + g][0] == t) g++;
-            for (size_t k = 0; k < t->terms.size(); ++k) {
-              const int lane = l + (int)(k % g), c = (int)(k / g);
-              slot(c, lane)[0] = (uint32_t)t->terms[k][0] * 8u;
-              slot(c, lane)[1] = (uint32_t)t->terms[k][1] * 8u;
-            }
-          } else {
-            for (size_t k = 0; k < t->terms.size(); ++k) {
-              const int c = 2 * q + (int)k;
-              slot(c, l)[0] = (uint32_t)t->terms[k][0] * 8u;
-              slot(c, l)[1] = (uint32_t)t->terms[k][1] * 8u;
-            }
-          }
-        }
-      // a group's non-first lanes store the same value to the same target: no sink needed
-      nsteps++;
-      pending.swap(deferred);
-    }
+    nsteps++;
   }
   return nsteps;
+}
+
+// Permute the LDS slots of the matrix values (L and the N | G | G' region) so that the matrix
+// operand reads of the solve steps are free of bank conflicts as far as possible: every value is
+// given a bank class (slot mod 32) that the other values read by the same instruction half do not
+// use (values read by both solves get the class that collides least), then the classes are mapped
+// to the region's slots.  All schedule records and assembly maps are rewritten.
+void layout_matrix_values(Plan& pl) {
+  const int nL = pl.nnzL, nM = pl.ZERO - pl.NB;
+  auto region = [&](int d) { return (d >= pl.LX && d < pl.LX + nL) ? 0 : ((d >= pl.NB && d < pl.ZERO) ? 1 : -1); };
+  // read groups: (table, step, c, half) -> values
+  std::vector<std::vector<int>> groups;
+  std::vector<std::vector<int>> uses(pl.LDS_N);
+  for (int w = 0; w < 2; ++w) {
+    const auto& t = w ? pl.bwd : pl.fwd;
+    const int ns = w ? pl.nbwd : pl.nfwd;
+    for (int s = 0; s < ns; ++s) {
+      const uint32_t* r = t.data() + (size_t)s * SOLVE_STEP_WORDS;
+      for (int c = 0; c < 8; ++c)
+        for (int h = 0; h < 2; ++h) {
+          std::vector<int> g;
+          for (int l = 32 * h; l < 32 * h + 32; ++l) {
+            const int d = (int)(r[(c / 2) * 256 + l * 4 + (c % 2) * 2] / 8u);
+            if (region(d) >= 0 && std::find(g.begin(), g.end(), d) == g.end()) g.push_back(d);
+          }
+          for (int d : g) uses[d].push_back((int)groups.size());
+          groups.push_back(std::move(g));
+        }
+    }
+  }
+  // capacity per (region, class)
+  int cap[2][32] = {};
+  const int rbase[2] = {pl.LX, pl.NB}, rsize[2] = {nL, nM};
+  for (int rg = 0; rg < 2; ++rg)
+    for (int k = 0; k < rsize[rg]; ++k) cap[rg][(rbase[rg] + k) % 32]++;
+  std::vector<int> cls(pl.LDS_N, -1);
+  // values without solve uses keep any class: first the constrained ones, biggest groups first
+  std::vector<int> order(groups.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return groups[a].size() > groups[b].size(); });
+  for (int gi : order) {
+    for (int d : groups[gi]) {
+      if (cls[d] >= 0) continue;
+      const int rg = region(d);
+      int best = -1, bestp = 1 << 30;
+      for (int c = 0; c < 32; ++c) {
+        if (cap[rg][c] == 0) continue;
+        int pen = 0;
+        for (int u : uses[d])
+          for (int o : groups[u])
+            if (o != d && cls[o] == c) pen++;
+        if (pen < bestp) bestp = pen, best = c;
+      }
+      cls[d] = best;
+      cap[rg][best]--;
+    }
+  }
+  // slots per class, then the permutation
+  std::vector<int> perm(pl.LDS_N);
+  for (int d = 0; d < pl.LDS_N; ++d) perm[d] = d;
+  for (int rg = 0; rg < 2; ++rg) {
+    std::vector<std::vector<int>> free_slots(32);
+    for (int k = 0; k < rsize[rg]; ++k) free_slots[(rbase[rg] + k) % 32].push_back(rbase[rg] + k);
+    std::vector<size_t> next(32, 0);
+    std::vector<int> rest;
+    for (int k = 0; k < rsize[rg]; ++k) {
+      const int d = rbase[rg] + k;
+      if (cls[d] >= 0)
+        perm[d] = free_slots[cls[d]][next[cls[d]]++];
+      else
+        rest.push_back(d);
+    }
+    std::vector<int> left;
+    for (int c = 0; c < 32; ++c)
+      for (size_t i = next[c]; i < free_slots[c].size(); ++i) left.push_back(free_slots[c][i]);
+    for (size_t i = 0; i < rest.size(); ++i) perm[rest[i]] = left[i];
+  }
+  auto mp = [&](uint32_t byteaddr) { return (uint32_t)perm[byteaddr / 8u] * 8u; };
+  for (int w = 0; w < 2; ++w) {
+    auto& t = w ? pl.bwd : pl.fwd;
+    for (auto& x : t) x = mp(x);  // every solve word is a byte address
+  }
+  for (int w = 0; w < 2; ++w) {
+    auto& t = w ? pl.tail : pl.fac;
+    const int ns = w ? pl.ntail : pl.nfac;
+    for (int s = 0; s < ns; ++s) {
+      uint32_t* r = t.data() + (size_t)s * FAC_STEP_WORDS;
+      for (int l = 0; l < 64; ++l) {
+        const uint32_t tgt = r[l] & META_TGT_MASK;
+        if (tgt / 8u < (uint32_t)pl.LDS_N) r[l] = (r[l] & ~META_TGT_MASK) | mp(tgt);
+      }
+      for (int k = 64; k < FAC_STEP_WORDS; ++k) r[k] = mp(r[k]);
+    }
+  }
+  for (auto& x : pl.slotP) x = (uint16_t)perm[x];
+  for (auto& x : pl.slotA) x = (uint16_t)perm[x];
+  std::vector<uint16_t> lc(nL);
+  for (int k = 0; k < nL; ++k) lc[perm[pl.LX + k] - pl.LX] = pl.Lcol[k];
+  pl.Lcol.swap(lc);
 }
 
 // padded per-slot ELL of `count` outputs; terms(e) lists (src, in) in summation order
@@ -696,9 +750,8 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     }
     if (k + 1 < T)
       for (int r = bs(k + 1); r < be(k + 1); r++) {
-        Task t;
+        Task t;  // accumulates into C_r (atomic adds)
         t.target = pl.CACC + r;
-        t.inplace = true;
         for (int x : lrow[r])
           if (x < bs(k)) t.terms.push_back({pl.LX + lpos(r, x), pl.W + x, 0});
         if (!t.terms.empty()) tasks.push_back(std::move(t));
@@ -720,9 +773,8 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     }
     if (k >= 1)
       for (int r = bs(k - 1); r < be(k - 1); r++) {
-        Task t;
+        Task t;  // accumulates into C_r (atomic adds)
         t.target = pl.CACC + r;
-        t.inplace = true;
         for (int z : lcol[r])
           if (z >= be(k)) t.terms.push_back({pl.LX + lpos(z, r), pl.W + z, 0});
         if (!t.terms.empty()) tasks.push_back(std::move(t));
@@ -731,6 +783,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   }
   pl.levels_fwd = T;
   pl.levels_bwd = T;
+  if (!getenv("MPCQP_NO_LAYOUT")) layout_matrix_values(pl);
 
   // ---- matrix structure for scaling / residuals
   pl.Ap.resize(n + 1);

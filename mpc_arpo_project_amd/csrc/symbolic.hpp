@@ -8,17 +8,20 @@
 // the GPU is purely numeric.
 //
 // Level schedules.  Factorization (left-looking, dot-product form on U = L D), forward solve
-// L w = b and backward solve L' x = w are each cut into levels of mutually independent "tasks"; a
-// task SETS one LDS slot  v[t] <- -sum_k prod(terms_k)  (2-factor terms for the solves, 3-factor
-// terms U_ik * U_jk * (1/D_k) for the factorization).  A task that updates its slot in place gets
-// the extra term (-1) * v[t], so the device never reads its target back.  A level is packed into
-// 64-lane "steps": a task gets an aligned group of g = 2^glog lanes, each lane accumulates <= C
-// terms and the group reduces with an xor butterfly; the group's first lane writes the slot.
+// L w = b and backward solve L' x = w are each cut into levels of mutually independent "tasks".
+// A factorization task SETS one LDS slot  v[t] <- -sum_k U_ik U_jk (1/D_k)  (a task that updates
+// its slot in place gets the extra term (-1) * v[t]); it gets an aligned group of g = 2^glog lanes,
+// each lane accumulates <= C terms, the group reduces with an xor butterfly and its first lane
+// writes the slot.  A solve task ACCUMULATES  v[t] += -sum_k v[a_k] v[b_k]: its terms are cut into
+// two-term segments that may sit in any lanes of any steps of the level, and every segment is
+// added to the target with an LDS atomic (targets are zeroed or hold the in-place value before
+// the level), so solve steps need no cross-lane reduction.
 //
 // Step records have a fixed stride (STEP_WORDS 32-bit words) so that the device computes no
-// record addresses: word [lane] is the lane's meta word, then MAXC rows of 64 lane records of
-// absolute LDS byte addresses: (a, b) pairs for the solves, (a, b, c, 0) quads for the
-// factorization.  Unused lanes / terms point at the image's ZERO slot.
+// record addresses: rows of 64 lane records of absolute LDS byte addresses -- the factorization's
+// meta words then (a, b, c, 0) quads, the solves' (a0, b0, a1, b1) segment quads then the
+// (t0, t1, t2, t3) target quads.  Unused terms point at the image's ZERO slot, unused segments
+// at the lane's sink slot.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -31,9 +34,9 @@ constexpr int FAC_MAXC = 4;     // terms per lane of a factorization step
 // factorization step: meta[64] | FAC_MAXC rows of 64 (a, b, c, 0) quads
 constexpr int FAC_STEP_WORDS = 64 + 64 * 4 * FAC_MAXC;
 // solve step: SOLVE_MAXC / 2 rows of 64 segment quads (a0, b0, a1, b1) | 64 target quads
-// (t0, t1, t2, t3) | meta[64]
+// (t0, t1, t2, t3); segment q of a lane is added to its target t_q with an LDS atomic
 constexpr int SOLVE_TERM_WORDS = 64 * 2 * SOLVE_MAXC;
-constexpr int SOLVE_STEP_WORDS = SOLVE_TERM_WORDS + 64 * 4 + 64;
+constexpr int SOLVE_STEP_WORDS = SOLVE_TERM_WORDS + 64 * 4;
 
 // meta word: per-lane fields, then the step-wide C and glog (identical in every lane)
 constexpr uint32_t META_TGT_MASK = 0x1ffffu;  // factorization: LDS byte address of the target
@@ -42,12 +45,6 @@ constexpr uint32_t META_HEAD = 1u << 20;
 constexpr uint32_t META_ISD = 1u << 21;       // factorization: target is D_j -> also write 1/D_j
 constexpr int META_C_SHIFT = 22;              // 4 bits: terms per lane in this step
 constexpr int META_SGLOG_SHIFT = 26;          // 3 bits: widest group log2 in this step
-// solve steps: a lane's 8 term slots are 4 two-term segments s0..s3 whose sums go to targets
-// t0..t3; FULL merges all four into t0 (one task, possibly spanning a lane group), H0 merges
-// s0 + s1 into t0, H1 merges s2 + s3 into t2.  Unused targets are the lane's sink slot.
-constexpr uint32_t META_FULL = 1u << 29;
-constexpr uint32_t META_H0 = 1u << 30;
-constexpr uint32_t META_H1 = 1u << 31;
 
 // Sparse mat-vec in padded per-slot ELL form for the residual checks: output element e sits on
 // lane e % 64, register slot r = e / 64; every used slot has exactly KMAX terms per lane (compile-
