@@ -86,7 +86,7 @@ struct KParams {
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
 // s_memtime deltas accumulated per wave in SGPRs, added to p.timing at the end of each instance.
-enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_NSLOT };
+enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_V0, T_V1, T_V2, T_NSLOT };
 #ifdef MPCQP_TIMING
 #define T_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define T_END(slot, v) tacc[slot] += __builtin_amdgcn_s_memtime() - (v)
@@ -313,11 +313,11 @@ __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops
 // reached at most once per ~12 steps.
 #ifdef EXP_NO_RECLOAD  // timing ablation: the three prefetched record sets are reused
 #define MPCQP_STEP(X)                                       \
-  ops.step(p.X);                                            \
+  ops.step(p.X, s);                                         \
   if (++s >= n) break;
 #else
 #define MPCQP_STEP(X)                                       \
-  ops.step(p.X);                                            \
+  ops.step(p.X, s);                                         \
   if (++s >= n) break;                                      \
   __builtin_amdgcn_sched_barrier(0);                        \
   Ops::load(rs, step_off<Ops>(n, s + 2), lane, p.X);        \
@@ -342,7 +342,7 @@ struct SolveOps {
   __device__ __forceinline__ static void load(Rsrc rs, int soff, uint32_t lane, Rec& r) {
     load_solve(rs, soff, lane, r);
   }
-  __device__ __forceinline__ void step(const Rec& r) const { solve_step(r, v); }
+  __device__ __forceinline__ void step(const Rec& r, int) const { solve_step(r, v); }
 };
 struct FacOps {
   typedef FacRec Rec;
@@ -352,7 +352,7 @@ struct FacOps {
   __device__ __forceinline__ static void load(Rsrc rs, int soff, uint32_t lane, Rec& r) {
     load_fac(rs, soff, lane, r);
   }
-  __device__ __forceinline__ void step(const Rec& r) const { fac_step(r, v, dshift); }
+  __device__ __forceinline__ void step(const Rec& r, int) const { fac_step(r, v, dshift); }
 };
 __device__ __forceinline__ void run_fac(const uint32_t* tbl, int nsteps, double* v, int lane,
                                         uint32_t dshift) {
@@ -1117,20 +1117,35 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
       if (i < m) v[wsz[r] + coff] = bz[r];
     }
-    for (int k = lane; k < P.nk; k += 64) v[P.W + k] = 0.0;  // the solve accumulates into W
+#pragma unroll
+    for (int r = 0; r < RN + RM; ++r)  // the solve accumulates into W
+      if (lane + 64 * r < P.nk) v[P.W + lane + 64 * r] = 0.0;
     LDS_FENCE();
     T_END(T_VEC, t_v0);
+    T_END(T_V0, t_v0);
     T_BEGIN(t_fw);
     run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
     T_END(T_FWD, t_fw);
     T_BEGIN(t_v1);
     prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
-    for (int k = lane; k < P.nk; k += 64) {
-      v[P.CACC + k] = v[P.W + k] * v[P.DINV + k];
-      v[P.W + k] = 0.0;
+    {
+      double wv[RN + RM], dv[RN + RM];
+#pragma unroll
+      for (int r = 0; r < RN + RM; ++r) {
+        const int k = lane + 64 * r < P.nk ? lane + 64 * r : 0;
+        wv[r] = v[P.W + k];
+        dv[r] = v[P.DINV + k];
+      }
+#pragma unroll
+      for (int r = 0; r < RN + RM; ++r)
+        if (lane + 64 * r < P.nk) {
+          v[P.CACC + lane + 64 * r] = wv[r] * dv[r];
+          v[P.W + lane + 64 * r] = 0.0;
+        }
     }
     LDS_FENCE();
     T_END(T_VEC, t_v1);
+    T_END(T_V1, t_v1);
     T_BEGIN(t_bw);
     run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
     T_END(T_BWD, t_bw);
@@ -1156,6 +1171,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     }
     LDS_FENCE();
     T_END(T_VEC, t_v2);
+    T_END(T_V2, t_v2);
     T_BEGIN(t_ck);
     can_check = chk && --chk_left == 0;  // iter % chk == 0
     if (can_check) chk_left = chk;

@@ -172,7 +172,7 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
     }
   const uint32_t zb = (uint32_t)pl.ZERO * 8u;
   int nsteps = 0;
-  for (size_t s0 = 0; s0 < segs.size(); s0 += 256) {
+  for (size_t s0 = 0; s0 < segs.size();) {
     const size_t s1 = std::min(segs.size(), s0 + 256);
     const size_t base = tbl.size();
     tbl.resize(base + SOLVE_STEP_WORDS, zb);
@@ -219,6 +219,7 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
       tg[l * 4 + q] = (uint32_t)g.target * 8u;
     }
     nsteps++;
+    s0 = s1;
   }
   return nsteps;
 }

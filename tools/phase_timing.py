@@ -15,7 +15,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.environ.get("MPCQP_TIMING_LIB") or os.path.join(REPO, "tools", "libmpcqp_timing.so")
 SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact", "resid", "term", "nchk", "adapt",
-         "scale_finish"]
+         "scale_finish", "vec_rhs", "vec_diag", "vec_update"]
 
 
 def build(extra=()):
@@ -76,7 +76,8 @@ def run(B=65536, steps=5, warmup=3, nx=20):
     out = {"B": B, "steps": steps, "kernel_ms_per_launch": kt / steps,
            "iters_per_solve": iters / n_inst, "factorizations_per_solve": t["nfact"] / n_inst,
            "cycles_per_solve": {k: t[k] / n_inst for k in SLOTS[:7]},
-           "cycles_per_iter": {k: t[k] / iters for k in ("fwd", "bwd", "vec", "check")},
+           "cycles_per_iter": {k: t[k] / iters for k in ("fwd", "bwd", "vec", "check", "vec_rhs", "vec_diag",
+                                                         "vec_update")},
            "cycles_per_factorization": t["factor"] / max(t["nfact"], 1),
            "cycles_per_check": {"resid": t["resid"] / max(t["nchk"], 1),
                                 "term": t["term"] / max(t["nchk"], 1),
