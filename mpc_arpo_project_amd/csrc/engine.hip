@@ -59,6 +59,7 @@ struct DevPlan {
   const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
   int n, m, nk, nnzP, nnzA, nnzL;
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
+  int NKS;  // 64-lane slots of the padded 1/D, W and C regions (symbolic.hpp NKP / 64 = RN + RM)
   // scaling index overlay (symbolic.hpp): 16-byte chunks copied to LDS at u16 offset SCI
   const uint4* sci_src;
   int SCI, S_ZERO, sci_n16, sci_eP, sci_eAt, sci_eA, sci_Pi, sci_Pc, sci_Ai, sci_Ac;
@@ -1076,15 +1077,18 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
-    wsx[r] = j < n ? (int)P.wsx[j] : P.ZERO + 1;
+    wsx[r] = j < n ? (int)P.wsx[j] : P.W + P.nk;  // junk slot
   }
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
-    wsz[r] = i < m ? (int)P.wsz[i] : P.ZERO + 1;
+    wsz[r] = i < m ? (int)P.wsz[i] : P.W + P.nk;
   }
   const int coff = P.CACC - P.W;  // rhs goes to the accumulator region, the solution comes back in W
-  const double sigma = p.s.sigma, alpha = p.s.alpha;
+  // loop constants held in VGPRs (an opaque copy: otherwise they are re-read from the kernel
+  // arguments inside the loop, with an lgkmcnt(0) wait that also drains the LDS queue)
+  double sigma = p.s.sigma, alpha = p.s.alpha, alpha_c = 1.0 - p.s.alpha;
+  asm volatile("" : "+v"(sigma), "+v"(alpha), "+v"(alpha_c));
   const int chk = p.s.check_termination;
   int ar_int = p.s.adaptive_rho_interval;
   if (p.s.adaptive_rho && ar_int == 0) ar_int = chk ? 4 * chk : 100;
@@ -1104,22 +1108,21 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);  // lands while the right-hand side is formed
     double xp[RN], zp[RM], bz[RM];
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
+    // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
-      const int j = lane + 64 * r;
       xp[r] = S.x[r];
-      if (j < n) v[wsx[r] + coff] = sigma * xp[r] - S.q[r];
+      v[wsx[r] + coff] = sigma * xp[r] - S.q[r];
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
-      const int i = lane + 64 * r;
       zp[r] = S.z[r];
       bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
-      if (i < m) v[wsz[r] + coff] = bz[r];
+      v[wsz[r] + coff] = bz[r];
     }
 #pragma unroll
-    for (int r = 0; r < RN + RM; ++r)  // the solve accumulates into W
-      if (lane + 64 * r < P.nk) v[P.W + lane + 64 * r] = 0.0;
+    for (int r = 0; r < RN + RM; ++r)  // the solve accumulates into W (NKP = 64 (RN + RM))
+      v[P.W + lane + 64 * r] = 0.0;
     LDS_FENCE();
     T_END(T_VEC, t_v0);
     T_END(T_V0, t_v0);
@@ -1132,16 +1135,14 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       double wv[RN + RM], dv[RN + RM];
 #pragma unroll
       for (int r = 0; r < RN + RM; ++r) {
-        const int k = lane + 64 * r < P.nk ? lane + 64 * r : 0;
-        wv[r] = v[P.W + k];
-        dv[r] = v[P.DINV + k];
+        wv[r] = v[P.W + lane + 64 * r];
+        dv[r] = v[P.DINV + lane + 64 * r];
       }
 #pragma unroll
-      for (int r = 0; r < RN + RM; ++r)
-        if (lane + 64 * r < P.nk) {
-          v[P.CACC + lane + 64 * r] = wv[r] * dv[r];
-          v[P.W + lane + 64 * r] = 0.0;
-        }
+      for (int r = 0; r < RN + RM; ++r) {
+        v[P.CACC + lane + 64 * r] = wv[r] * dv[r];
+        v[P.W + lane + 64 * r] = 0.0;
+      }
     }
     LDS_FENCE();
     T_END(T_VEC, t_v1);
@@ -1153,18 +1154,16 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     // x, z, y updates (auxil.c update_x / update_z / update_y)
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
-      const int j = lane + 64 * r;
-      const double xt = j < n ? v[wsx[r]] : 0.0;
-      S.x[r] = alpha * xt + (1.0 - alpha) * xp[r];
+      const double xt = v[wsx[r]];  // the junk slot reads back 0
+      S.x[r] = alpha * xt + alpha_c * xp[r];
       dx[r] = S.x[r] - xp[r];
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
-      const int i = lane + 64 * r;
-      const double nu = i < m ? v[wsz[r]] : 0.0;
+      const double nu = v[wsz[r]];
       const double ri = rinv_of(S, r);
       const double zt = bz[r] + ri * nu;
-      const double zr = alpha * zt + (1.0 - alpha) * zp[r];
+      const double zr = alpha * zt + alpha_c * zp[r];
       S.z[r] = dmind(dmaxd(zr + ri * S.y[r], S.l[r]), S.u[r]);
       dy[r] = rvec_of(S, r) * (zr - S.z[r]);
       S.y[r] = S.y[r] + dy[r];
@@ -1341,11 +1340,12 @@ kernel_fn pick() {
 
 // RN = ceil(n/64) and RM = ceil(m/64) rounded up to the instantiated buckets
 kernel_fn select_kernel(int n, int m) {
-  const int rn = (n + 63) / 64, rm = (m + 63) / 64;
-  if (rn <= 2 && rm <= 4) return pick<2, 4>();
+  int rn = 0, rm = 0;
+  if (!kernel_bucket(n, m, rn, rm)) return nullptr;
+  if (rn == 2) return pick<2, 4>();
 #ifndef MPCQP_ONLY_SMALL
-  if (rn <= 4 && rm <= 8) return pick<4, 8>();
-  if (rn <= 8 && rm <= 16) return pick<8, 16>();
+  if (rn == 4) return pick<4, 8>();
+  if (rn == 8) return pick<8, 16>();
 #endif
   return nullptr;
 }
@@ -1533,7 +1533,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
     dp.nnzL = pl.nnzL;
     dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.CACC = pl.CACC, dp.ZERO = pl.ZERO;
-    dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N;
+    dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N, dp.NKS = pl.NKP / 64;
     dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
     dp.sci_src = (const uint4*)(b + o_sci), dp.SCI = pl.SCI, dp.S_ZERO = pl.S_ZERO;
     dp.sci_n16 = (int)(pl.sci_block.size() / 8);

@@ -542,10 +542,18 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   }
   // ---- LDS layout (doubles)
   pl.LX = 0;
+  {
+    int rn = 0, rm = 0;
+    if (!kernel_bucket(n, m, rn, rm)) {
+      pl.error = "problem too large for the engine's register-slot buckets";
+      return false;
+    }
+    pl.NKP = 64 * (rn + rm);
+  }
   pl.DINV = pl.nnzL;
-  pl.W = pl.DINV + nk;
-  pl.CACC = pl.W + nk;
-  pl.NB = pl.CACC + nk;
+  pl.W = pl.DINV + pl.NKP;
+  pl.CACC = pl.W + pl.NKP;
+  pl.NB = pl.CACC + pl.NKP;
   std::vector<int> noff(nk + 1, 0), goff(nk + 1, 0), gpoff(nk + 1, 0);
   for (int r = 0; r < nk; r++) {
     noff[r + 1] = noff[r] + (int)reach[r].size();

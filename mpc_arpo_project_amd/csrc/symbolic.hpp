@@ -66,12 +66,30 @@ struct Ell {
   std::vector<uint16_t> src, in;
 };
 
+// Register-slot bucket of the engine kernel: RN >= ceil(n / 64) slots for n-vectors, RM >= ceil(m /
+// 64) for m-vectors, from the instantiated set (2,4), (4,8), (8,16), with RN + RM > nk / 64 (a junk
+// slot).  false if no bucket fits.
+inline bool kernel_bucket(int n, int m, int& rn, int& rm) {
+  const int need_n = (n + 63) / 64, need_m = (m + 63) / 64, need_k = (n + m) / 64 + 1;
+  for (int b = 2; b <= 8; b *= 2)
+    if (need_n <= b && need_m <= 2 * b && 3 * b >= need_k) {
+      rn = b, rm = 2 * b;
+      return true;
+    }
+  return false;
+}
+
 struct Plan {
   int n = 0, m = 0, nk = 0, nnzP = 0, nnzA = 0, nnzL = 0;
   std::vector<int32_t> perm, pinv, Lp, Li, etree;
   // LDS layout, in doubles: L | 1/D | W (solve vector) | C (accumulators) | N (negated block
   // inverses) | G | G' | ZERO ONE MONE pad | SINK (64 slots)
   int LX = 0, DINV = 0, W = 0, CACC = 0, NB = 0, GB = 0, GPB = 0, ZERO = 0, ONE = 0, MONE = 0;
+  // the 1/D, W and C regions are NKP = 64 * (RN + RM) doubles long (the kernel's register-slot bucket,
+  // kernel_bucket below): whole 64-lane slots, so the per-iteration vector passes store
+  // unconditionally, and slot nk of each (the "junk" slot) takes the stores of lanes past the end of x
+  // or z (W[nk] is zeroed every iteration and read back as 0)
+  int NKP = 0;
   int SINK = 0;
   int LDS_N = 0;
   // blocked substitution: contiguous blocks of the permuted order
