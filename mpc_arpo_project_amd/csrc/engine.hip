@@ -252,6 +252,8 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
 #pragma unroll
 #ifdef EXP_NO_LDSREAD  // timing ablation: operands from the record words instead of LDS
   for (int c = 0; c < 8; ++c) x[c] = (double)r.a[c], y[c] = (double)r.b[c];
+#elif defined(EXP_NO_MATREAD)  // timing ablation: matrix operands not read from LDS
+  for (int c = 0; c < 8; ++c) x[c] = (double)r.a[c], y[c] = lds_ld(v, r.b[c]);
 #else
   for (int c = 0; c < 8; ++c) x[c] = lds_ld(v, r.a[c]), y[c] = lds_ld(v, r.b[c]);
 #endif
@@ -261,10 +263,20 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
   const double n1 = fma(-x[3], y[3], -(x[2] * y[2]));
   const double n2 = fma(-x[5], y[5], -(x[4] * y[4]));
   const double n3 = fma(-x[7], y[7], -(x[6] * y[6]));
+#if defined(EXP_WRITE_NOT_ADD)  // timing ablation: plain stores instead of LDS atomics
+  lds_st(v, r.t0, n0);
+  lds_st(v, r.t1, n1);
+  lds_st(v, r.t2, n2);
+  lds_st(v, r.t3, n3);
+#elif defined(EXP_TWO_ADDS)  // timing ablation: two atomics per lane
+  lds_add(r.t0, n0 + n1);
+  lds_add(r.t2, n2 + n3);
+#else
   lds_add(r.t0, n0);
   lds_add(r.t1, n1);
   lds_add(r.t2, n2);
   lds_add(r.t3, n3);
+#endif
   LDS_FENCE();
 }
 // One factorization step: v[t] <- -sum_c v[a_c] v[b_c] v[c_c]; a D_j target also writes 1/D_j at
@@ -389,6 +401,7 @@ struct Inst {
   double c, cinv, rho;
   double rv_eq, ri_eq, ri_in, ri_free;  // rho_vec / rho_inv_vec values per class
   double pri_res, dua_res;
+  double Dinv[RN], Einv[RM];  // inverse scalings (termination checks), 1 past the end of x / z
 };
 
 // per-wave scratch slab layout (doubles)
@@ -630,16 +643,14 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   double* xb = v + P.W;
   double* yb = v + P.W + n;
   LDS_FENCE();
+  // unconditional stores: x's slots past n land in y's range and are overwritten by the y stores
+  // that follow (a wave's LDS stores complete in order); y's slots past m stay inside the padded
+  // W region (n + 64 RM <= 64 (RN + RM) = NKP)
 #pragma unroll
-  for (int r = 0; r < RN; ++r) {
-    const int i = lane + 64 * r;
-    if (i < n) xb[i] = S.x[r];
-  }
+  for (int r = 0; r < RN; ++r) xb[lane + 64 * r] = S.x[r];
+  LDS_FENCE();
 #pragma unroll
-  for (int r = 0; r < RM; ++r) {
-    const int i = lane + 64 * r;
-    if (i < m) yb[i] = S.y[r];
-  }
+  for (int r = 0; r < RM; ++r) yb[lane + 64 * r] = S.y[r];
   LDS_FENCE();
   double pr = 0.0, dr = 0.0;
   ell_mv<RM, ELL_KA>(P.eA, sb.vA, xb, R.Ax, lane);  // padding terms are 0 * x
@@ -648,13 +659,13 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
-    if (i < m) pr = dmaxd(pr, fabs(sb.Einv[i] * (R.Ax[r] - S.z[r])));
+    if (i < m) pr = dmaxd(pr, fabs(S.Einv[r] * (R.Ax[r] - S.z[r])));
     if (i >= m) R.Ax[r] = 0.0;
   }
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
-    if (j < n) dr = dmaxd(dr, fabs(sb.Dinv[j] * ((S.q[r] + R.Px[r]) + R.Aty[r])));
+    if (j < n) dr = dmaxd(dr, fabs(S.Dinv[r] * ((S.q[r] + R.Px[r]) + R.Aty[r])));
     if (j >= n) R.Px[r] = 0.0, R.Aty[r] = 0.0;
   }
   S.pri_res = wave_max(pr);
@@ -703,7 +714,7 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
     if (j < P.n) {
       double s = 0.0;
       for (int k = P.Ap[j]; k < P.Ap[j + 1]; ++k) s += sb.As[k] * yb[P.Ai[k]];
-      mx = dmaxd(mx, fabs(s * sb.Dinv[j]));
+      mx = dmaxd(mx, fabs(s * S.Dinv[r]));
     }
   }
   mx = wave_max(mx);
@@ -743,7 +754,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
     if (j < P.n) {
       double s = 0.0;
       for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) s += sb.Ps[P.Psk[e]] * xb[P.Pso[e]];
-      mx = dmaxd(mx, fabs(s * sb.Dinv[j]));
+      mx = dmaxd(mx, fabs(s * S.Dinv[r]));
     }
   }
   mx = wave_max(mx);
@@ -755,7 +766,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
     if (i < P.m) {
       double s = 0.0;
       for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) s += sb.As[P.Ark[q]] * xb[P.Arj[q]];
-      s *= sb.Einv[i];
+      s *= S.Einv[r];
       if ((S.u[r] < thr && s > eps * nrm) || (S.l[r] > -thr && s < -eps * nrm)) bad = 1;
     }
   }
@@ -776,7 +787,7 @@ __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>&
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
     if (i < P.m) {
-      const double ei = sb.Einv[i];
+      const double ei = S.Einv[r];
       zn = dmaxd(zn, fabs(ei * S.z[r]));
       axn = dmaxd(axn, fabs(ei * R.Ax[r]));
     }
@@ -785,7 +796,7 @@ __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>&
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
     if (j < P.n) {
-      const double di = sb.Dinv[j];
+      const double di = S.Dinv[r];
       qn = dmaxd(qn, fabs(di * S.q[r]));
       atn = dmaxd(atn, fabs(di * R.Aty[r]));
       pxn = dmaxd(pxn, fabs(di * R.Px[r]));
@@ -973,17 +984,19 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
     S.ct |= t << (2 * r);
     S.l[r] = E[r] * S.l[r];
     S.u[r] = E[r] * S.u[r];
+    S.Einv[r] = 1. / E[r];
     if (i < m) {
       sb.E[i] = E[r];
-      sb.Einv[i] = 1. / E[r];
+      sb.Einv[i] = S.Einv[r];
     }
   }
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
+    S.Dinv[r] = 1. / D[r];
     if (j < n) {
       sb.D[j] = D[r];
-      sb.Dinv[j] = 1. / D[r];
+      sb.Dinv[j] = S.Dinv[r];
     }
   }
   // park scaled P, A for residuals / refactorization (per-wave slab)
