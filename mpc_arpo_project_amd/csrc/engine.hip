@@ -1343,8 +1343,8 @@ int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return (e && *e) ? atoi(e) : dflt;
 }
-int cap_m() { return env_int("MPCQP_CAPM", 128); }
-int cap_w() { return env_int("MPCQP_CAPW", 384); }
+int cap_m() { return env_int("MPCQP_CAPM", 0); }  // 0: chosen per structure
+int cap_w() { return env_int("MPCQP_CAPW", 0); }
 
 template <int RN, int RM>
 kernel_fn pick() {
@@ -1452,7 +1452,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   h->set = *s;
   h->B = batch;
   h->stream = (hipStream_t)stream;
-  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, h->plan, cap_m(), cap_w())) {
+  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, h->plan, cap_m(), cap_w())) {
     std::string e = h->plan.error;
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, e);
@@ -1761,7 +1761,7 @@ int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t
                   int32_t* nnzL, int32_t* stats) {
   if (!st || !nnzL) return fail(MPCQP_E_INVALID, "null argument");
   Plan pl;
-  if (!build_plan(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w()))
+  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   const int cap = *nnzL;
   *nnzL = pl.nnzL;

@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <array>
 #include <numeric>
+#include <map>
+#include <mutex>
 #include <unordered_map>
 
 namespace mpcqp {
@@ -360,6 +362,69 @@ bool make_ell(int count, int kmax, F terms, Ell& e) {
 }
 
 }  // namespace
+
+// An accumulation term of a blocked substitution: C[target] -= v[a] v[b], allowed in any level of
+// [lo, hi] (the levels after its source block is final and before its target block is computed).
+struct AccTerm {
+  int target;
+  std::array<int, 3> term;
+  int lo, hi;
+};
+
+// Distribute the accumulation terms over the levels so that as few levels as possible overflow one
+// 64-lane step (256 two-term segments): level by level, the terms whose last allowed level this is
+// go in first, then, earliest deadline first, terms that could still wait, while the level has
+// room.  Terms of one target placed in the same level form one task (segments = ceil(terms / 2)).
+std::vector<std::vector<Task>> place_accumulations(std::vector<std::vector<Task>> fixed,
+                                                   const std::vector<AccTerm>& acc) {
+  const int T = (int)fixed.size();
+  constexpr int CAP = 256;
+  std::vector<int> order(acc.size());
+  for (size_t i = 0; i < acc.size(); ++i) order[i] = (int)i;
+  // deadline, then source level, then target: deterministic
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    if (acc[a].hi != acc[b].hi) return acc[a].hi < acc[b].hi;
+    if (acc[a].lo != acc[b].lo) return acc[a].lo < acc[b].lo;
+    return acc[a].target < acc[b].target;
+  });
+  std::vector<char> done(acc.size(), 0);
+  for (int p = 0; p < T; ++p) {
+    int segs = 0;
+    for (const Task& t : fixed[p]) segs += ((int)t.terms.size() + 1) / 2;
+    std::vector<int> tidx;  // target -> index of its accumulation task in fixed[p]
+    std::vector<int> tslot;
+    auto add = [&](int i) {
+      const AccTerm& a = acc[i];
+      size_t q = 0;
+      while (q < tslot.size() && tslot[q] != a.target) ++q;
+      if (q == tslot.size()) {
+        Task t;
+        t.target = a.target;
+        fixed[p].push_back(t);
+        tslot.push_back(a.target);
+        tidx.push_back((int)fixed[p].size() - 1);
+      }
+      Task& t = fixed[p][tidx[q]];
+      const int before = ((int)t.terms.size() + 1) / 2;
+      t.terms.push_back(a.term);
+      segs += ((int)t.terms.size() + 1) / 2 - before;
+      done[i] = 1;
+    };
+    auto cost = [&](int i) {  // extra segments if term i joined level p
+      for (size_t q = 0; q < tslot.size(); ++q)
+        if (tslot[q] == acc[i].target) return (fixed[p][tidx[q]].terms.size() % 2) ? 0 : 1;
+      return 1;
+    };
+    for (int i : order)
+      if (!done[i] && acc[i].hi == p) add(i);
+    const int room = CAP * std::max(1, (segs + CAP - 1) / CAP);
+    for (int i : order)
+      if (!done[i] && acc[i].lo <= p && acc[i].hi > p && segs + cost(i) <= room) add(i);
+  }
+  for (size_t i = 0; i < acc.size(); ++i)
+    if (!done[i]) fixed[acc[i].hi].push_back(Task{acc[i].target, false, false, {acc[i].term}});  // unreachable
+  return fixed;
+}
 
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                 const int32_t* Ai, Plan& pl, int capM, int capW) {
@@ -743,52 +808,52 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     }
     pl.ntail += pack_fac_level(tasks, pl, pl.tail);
   }
-  // ---- forward solve (input C = rhs, output W): level k
+  // ---- forward solve (input C = rhs, output W), level k computes block k:
   //   W_r = sum_{r2 in reach(r) U {r}} M_{r r2} C_{r2} - sum_{x in block k-1} G_{r x} W_x   (r in block k)
-  //   C_r -= sum_{x in blocks <= k-1} L_{r x} W_x                 (r in block k+1: one merged task,
-  //                                                                  just in time for level k+1)
-  for (int k = 0; k < T; k++) {
-    std::vector<Task> tasks;
-    for (int r = bs(k); r < be(k); r++) {
-      Task t;
-      t.target = pl.W + r;
-      for (int r2 : reach[r]) t.terms.push_back({nslot(r, r2), pl.CACC + r2, 0});
-      t.terms.push_back({pl.MONE, pl.CACC + r, 0});
-      for (int x : gpat[r]) t.terms.push_back({gslot(r, x), pl.W + x, 0});
-      tasks.push_back(std::move(t));
-    }
-    if (k + 1 < T)
-      for (int r = bs(k + 1); r < be(k + 1); r++) {
-        Task t;  // accumulates into C_r (atomic adds)
-        t.target = pl.CACC + r;
-        for (int x : lrow[r])
-          if (x < bs(k)) t.terms.push_back({pl.LX + lpos(r, x), pl.W + x, 0});
-        if (!t.terms.empty()) tasks.push_back(std::move(t));
-      }
-    pl.nfwd += pack_solve_level(tasks, pl, pl.fwd);
-  }
-  // ---- backward solve (input C = D^-1 W, output W): blocks in reverse, level k
+  //   C_r -= L_{r x} W_x  for r in block b and x in blocks <= b - 2: an accumulation term that may
+  //          run in any level from blk(x) + 1 to b - 1 (place_accumulations balances the levels)
+  // ---- backward solve (input C = D^-1 W, output W): blocks in reverse, level T-1-k computes block k:
   //   W_r = sum_{r2: r in reach(r2) or r2 == r} M_{r2 r} C_{r2} - sum_{z in block k+1} G'_{r z} W_z
-  //   C_r -= sum_{z in blocks >= k+1} L_{z r} W_z                 (r in block k-1, merged)
-  for (int k = T - 1; k >= 0; k--) {
-    std::vector<Task> tasks;
-    for (int r = bs(k); r < be(k); r++) {
-      Task t;
-      t.target = pl.W + r;
-      for (int r2 : rtr[r]) t.terms.push_back({nslot(r2, r), pl.CACC + r2, 0});
-      t.terms.push_back({pl.MONE, pl.CACC + r, 0});
-      for (int z : gppat[r]) t.terms.push_back({gpslot(r, z), pl.W + z, 0});
-      tasks.push_back(std::move(t));
-    }
-    if (k >= 1)
-      for (int r = bs(k - 1); r < be(k - 1); r++) {
-        Task t;  // accumulates into C_r (atomic adds)
-        t.target = pl.CACC + r;
-        for (int z : lcol[r])
-          if (z >= be(k)) t.terms.push_back({pl.LX + lpos(z, r), pl.W + z, 0});
-        if (!t.terms.empty()) tasks.push_back(std::move(t));
+  //   C_r -= L_{z r} W_z  for r in block b and z in blocks >= b + 2 (any level from the one after
+  //          z's block to the one before b's)
+  {
+    std::vector<std::vector<Task>> fixed(T);
+    std::vector<AccTerm> acc;
+    for (int k = 0; k < T; k++)
+      for (int r = bs(k); r < be(k); r++) {
+        Task t;
+        t.target = pl.W + r;
+        for (int r2 : reach[r]) t.terms.push_back({nslot(r, r2), pl.CACC + r2, 0});
+        t.terms.push_back({pl.MONE, pl.CACC + r, 0});
+        for (int x : gpat[r]) t.terms.push_back({gslot(r, x), pl.W + x, 0});
+        fixed[k].push_back(std::move(t));
+        if (k >= 2)
+          for (int x : lrow[r])
+            if (x < bs(k - 1)) acc.push_back({pl.CACC + r, {pl.LX + lpos(r, x), pl.W + x, 0}, blk[x] + 1, k - 1});
       }
-    pl.nbwd += pack_solve_level(tasks, pl, pl.bwd);
+    std::vector<std::vector<Task>> lv = place_accumulations(fixed, acc);
+    for (int k = 0; k < T; k++) pl.nfwd += pack_solve_level(lv[k], pl, pl.fwd);
+  }
+  {
+    std::vector<std::vector<Task>> fixed(T);
+    std::vector<AccTerm> acc;
+    for (int k = T - 1; k >= 0; k--) {
+      const int pos = T - 1 - k;
+      for (int r = bs(k); r < be(k); r++) {
+        Task t;
+        t.target = pl.W + r;
+        for (int r2 : rtr[r]) t.terms.push_back({nslot(r2, r), pl.CACC + r2, 0});
+        t.terms.push_back({pl.MONE, pl.CACC + r, 0});
+        for (int z : gppat[r]) t.terms.push_back({gpslot(r, z), pl.W + z, 0});
+        fixed[pos].push_back(std::move(t));
+        if (k + 2 < T)
+          for (int z : lcol[r])
+            if (z >= be(k + 1))
+              acc.push_back({pl.CACC + r, {pl.LX + lpos(z, r), pl.W + z, 0}, T - 1 - blk[z] + 1, pos - 1});
+      }
+    }
+    std::vector<std::vector<Task>> lv = place_accumulations(fixed, acc);
+    for (int p = 0; p < T; p++) pl.nbwd += pack_solve_level(lv[p], pl, pl.bwd);
   }
   pl.levels_fwd = T;
   pl.levels_bwd = T;
@@ -880,6 +945,55 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     }
   }
   return true;
+}
+
+}  // namespace mpcqp
+
+namespace mpcqp {
+
+bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                      const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu,
+                      int max_per_cu) {
+  if (capM > 0 && capW > 0) return build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW);
+  if (n <= 0 || m < 0) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);
+  // structure key
+  std::vector<int32_t> key;
+  key.push_back(n), key.push_back(m), key.push_back(lds_per_cu), key.push_back(max_per_cu);
+  key.insert(key.end(), Pp, Pp + n + 1);
+  key.insert(key.end(), Pi, Pi + Pp[n]);
+  key.insert(key.end(), Ap, Ap + n + 1);
+  key.insert(key.end(), Ai, Ai + Ap[n]);
+  static std::mutex mu;
+  static std::map<std::vector<int32_t>, std::pair<int, int>> memo;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = memo.find(key);
+    if (it != memo.end()) return build_plan(n, m, Pp, Pi, Ap, Ai, plan, it->second.first, it->second.second);
+  }
+  static const int CM[] = {96, 112, 128, 144, 160, 176, 192, 224, 256};
+  static const int CW[] = {320, 352, 384, 416, 448, 480};
+  bool found = false;
+  int best[4] = {0, 0, 0, 0};  // -per_cu, solve steps, fac steps, lds bytes
+  int bm = 128, bw = 384;
+  for (int cm : CM)
+    for (int cw : CW) {
+      Plan pl;
+      if (!build_plan(n, m, Pp, Pi, Ap, Ai, pl, cm, cw)) continue;
+      const int lds = ((pl.LDS_N + 1) & ~1) * 8;
+      const int per_cu = std::min(max_per_cu, lds_per_cu / std::max(lds, 1));
+      const int sc[4] = {-per_cu, pl.nfwd + pl.nbwd, pl.nfac + pl.ntail, lds};
+      if (!found || std::lexicographical_compare(sc, sc + 4, best, best + 4)) {
+        found = true;
+        std::copy(sc, sc + 4, best);
+        bm = cm, bw = cw;
+      }
+    }
+  if (!found) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);  // reports the error
+  {
+    std::lock_guard<std::mutex> g(mu);
+    memo[key] = {bm, bw};
+  }
+  return build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw);
 }
 
 }  // namespace mpcqp

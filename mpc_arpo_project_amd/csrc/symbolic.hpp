@@ -130,4 +130,12 @@ struct Plan {
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                 const int32_t* Ai, Plan& plan, int capM = 128, int capW = 384);
 
+// build_plan with the block caps chosen per structure: over a grid of (capM, capW), the plan with
+// the most instances per CU (LDS image within lds_per_cu / k for k <= max_per_cu), then the fewest
+// solve steps per ADMM iteration, then the fewest factorization steps.  capM / capW > 0 force a
+// single build.  Results are memoised per structure within the process.
+bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                      const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu = 163840,
+                      int max_per_cu = 4);
+
 }  // namespace mpcqp
