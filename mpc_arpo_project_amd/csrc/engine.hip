@@ -630,7 +630,9 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
     if (i < P.m) v[P.slotRho[i]] = -rinv_of(S, r);
   }
   LDS_FENCE();
+#ifndef EXP_SKIP_FACTOR  // timing ablation
   run_factor(p, v, lane);
+#endif
 }
 
 // update_info: scaled Ax, Px, A'y and the unscaled residual norms (auxil.c compute_pri_res /
@@ -906,7 +908,11 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
   }
   S.c = 1.0;
   LDS_FENCE();
+#ifdef EXP_SKIP_SCALE  // timing ablation: no Ruiz passes
+  for (int it = 0; it < 0; ++it) {
+#else
   for (int it = 0; it < p.s.scaling; ++it) {
+#endif
     // compute_inf_norm_cols_KKT: columns of [P A'; A 0] (P symmetric from its upper triangle)
     double dp[RN], da[RN], er[RM], dt[RN], et[RM];
     ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dp, lane);
@@ -1122,6 +1128,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     double xp[RN], zp[RM], bz[RM];
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
     // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
+#ifndef EXP_SKIP_RHS  // timing ablations (tools/ablate_fixed.sh): EXP_NOCHECK + EXP_SKIP_*
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       xp[r] = S.x[r];
@@ -1136,14 +1143,23 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #pragma unroll
     for (int r = 0; r < RN + RM; ++r)  // the solve accumulates into W (NKP = 64 (RN + RM))
       v[P.W + lane + 64 * r] = 0.0;
+#else
+#pragma unroll
+    for (int r = 0; r < RN; ++r) xp[r] = S.x[r];
+#pragma unroll
+    for (int r = 0; r < RM; ++r) zp[r] = S.z[r], bz[r] = S.y[r];
+#endif
     LDS_FENCE();
     T_END(T_VEC, t_v0);
     T_END(T_V0, t_v0);
     T_BEGIN(t_fw);
+#ifndef EXP_SKIP_FWD
     run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
+#endif
     T_END(T_FWD, t_fw);
     T_BEGIN(t_v1);
     prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
+#ifndef EXP_SKIP_DIAG
     {
       double wv[RN + RM], dv[RN + RM];
 #pragma unroll
@@ -1157,23 +1173,34 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         v[P.W + lane + 64 * r] = 0.0;
       }
     }
+#endif
     LDS_FENCE();
     T_END(T_VEC, t_v1);
     T_END(T_V1, t_v1);
     T_BEGIN(t_bw);
+#ifndef EXP_SKIP_BWD
     run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
+#endif
     T_END(T_BWD, t_bw);
     T_BEGIN(t_v2);
     // x, z, y updates (auxil.c update_x / update_z / update_y)
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
+#ifdef EXP_SKIP_UPDATE
+      const double xt = 0.0;
+#else
       const double xt = v[wsx[r]];  // the junk slot reads back 0
+#endif
       S.x[r] = alpha * xt + alpha_c * xp[r];
       dx[r] = S.x[r] - xp[r];
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
+#ifdef EXP_SKIP_UPDATE
+      const double nu = 0.0;
+#else
       const double nu = v[wsz[r]];
+#endif
       const double ri = rinv_of(S, r);
       const double zt = bz[r] + ri * nu;
       const double zr = alpha * zt + alpha_c * zp[r];
@@ -1205,6 +1232,11 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       T_BEGIN(t_tm);
       status = check_termination(p, S, R, dy, dx, sb, v, lane, false);
       T_END(T_TERM, t_tm);
+#ifdef EXP_CHECK_NOEXIT  // timing ablation: checks computed, 125 iterations regardless
+      if (iter > 100) break;
+      status = 0;
+      continue;
+#endif
       if (status != 0) break;
       status = MPCQP_UNSOLVED;
     }

@@ -363,6 +363,48 @@ bool make_ell(int count, int kmax, F terms, Ell& e) {
 
 }  // namespace
 
+// Diagnostic (MPCQP_DUMP_CONFLICTS): modelled LDS cycles of each solve step -- reads: per instruction
+// half (32 lanes) the largest number of distinct addresses sharing a bank (double slot mod 32);
+// atomics: per 16-lane group the largest number of lanes whose targets share a bank (slot mod 16).
+void dump_conflicts(const Plan& pl) {
+  for (int w = 0; w < 2; ++w) {
+    const auto& t = w ? pl.bwd : pl.fwd;
+    const int ns = w ? pl.nbwd : pl.nfwd;
+    long tot_a = 0, tot_b = 0, tot_t = 0;
+    for (int s = 0; s < ns; ++s) {
+      const uint32_t* r = t.data() + (size_t)s * SOLVE_STEP_WORDS;
+      int ca = 0, cb = 0, ct = 0, used = 0;
+      for (int c = 0; c < 8; ++c)
+        for (int ab = 0; ab < 2; ++ab)
+          for (int h = 0; h < 2; ++h) {
+            std::vector<std::vector<uint32_t>> bank(32);
+            for (int l = 32 * h; l < 32 * h + 32; ++l) {
+              const uint32_t d = r[(c / 2) * 256 + l * 4 + (c % 2) * 2 + ab] / 8u;
+              auto& b = bank[d % 32];
+              if (std::find(b.begin(), b.end(), d) == b.end()) b.push_back(d);
+            }
+            size_t mx = 1;
+            for (auto& b : bank) mx = std::max(mx, b.size());
+            (ab ? cb : ca) += (int)mx;
+          }
+      for (int q = 0; q < 4; ++q)
+        for (int g = 0; g < 4; ++g) {
+          int cnt[16] = {};
+          for (int l = 16 * g; l < 16 * g + 16; ++l) {
+            const uint32_t d = r[SOLVE_TERM_WORDS + l * 4 + q] / 8u;
+            cnt[d % 16]++;
+            if (d < (uint32_t)pl.SINK || d >= (uint32_t)pl.SINK + 64) used++;
+          }
+          ct += *std::max_element(cnt, cnt + 16);
+        }
+      fprintf(stderr, "%s step %d: segs %d  read cycles mat %d vec %d (min 32 each)  atomic group-cycles %d (min 16)\n",
+              w ? "bwd" : "fwd", s, used, ca, cb, ct);
+      tot_a += ca, tot_b += cb, tot_t += ct;
+    }
+    fprintf(stderr, "%s total: mat %ld vec %ld atomic %ld over %d steps\n", w ? "bwd" : "fwd", tot_a, tot_b, tot_t, ns);
+  }
+}
+
 // An accumulation term of a blocked substitution: C[target] -= v[a] v[b], allowed in any level of
 // [lo, hi] (the levels after its source block is final and before its target block is computed).
 struct AccTerm {
@@ -858,6 +900,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   pl.levels_fwd = T;
   pl.levels_bwd = T;
   if (!getenv("MPCQP_NO_LAYOUT")) layout_matrix_values(pl);
+  if (getenv("MPCQP_DUMP_CONFLICTS")) dump_conflicts(pl);
 
   // ---- matrix structure for scaling / residuals
   pl.Ap.resize(n + 1);
