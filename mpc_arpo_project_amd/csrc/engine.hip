@@ -704,21 +704,15 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
   double* yb = v + P.W + P.n;
   LDS_FENCE();
 #pragma unroll
-  for (int r = 0; r < RM; ++r) {
-    const int i = lane + 64 * r;
-    if (i < P.m) yb[i] = dy[r];
-  }
+  for (int r = 0; r < RM; ++r) yb[lane + 64 * r] = dy[r];  // slots past m: W padding
   LDS_FENCE();
+  // A' dy by the residual ELL (same term order as the CSC column traversal, loads batched)
+  double aty[RN];
+  ell_mv<RN, ELL_KAT>(P.eAt, sb.vAt, yb, aty, lane);
   double mx = 0.0;
 #pragma unroll
-  for (int r = 0; r < RN; ++r) {
-    const int j = lane + 64 * r;
-    if (j < P.n) {
-      double s = 0.0;
-      for (int k = P.Ap[j]; k < P.Ap[j + 1]; ++k) s += sb.As[k] * yb[P.Ai[k]];
-      mx = dmaxd(mx, fabs(s * S.Dinv[r]));
-    }
-  }
+  for (int r = 0; r < RN; ++r)
+    if (lane + 64 * r < P.n) mx = dmaxd(mx, fabs(aty[r] * S.Dinv[r]));
   mx = wave_max(mx);
   return mx < eps * nrm;
 }
@@ -744,31 +738,24 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
   double* xb = v + P.W;
   LDS_FENCE();
 #pragma unroll
-  for (int r = 0; r < RN; ++r) {
-    const int j = lane + 64 * r;
-    if (j < P.n) xb[j] = dx[r];
-  }
+  for (int r = 0; r < RN; ++r) xb[lane + 64 * r] = dx[r];  // slots past n: inside the W region
   LDS_FENCE();
+  // P dx and A dx by the residual ELLs (same term orders as the symmetric / CSR traversals)
+  double pdx[RN];
+  ell_mv<RN, ELL_KP>(P.eP, sb.vP, xb, pdx, lane);
   double mx = 0.0;
 #pragma unroll
-  for (int r = 0; r < RN; ++r) {
-    const int j = lane + 64 * r;
-    if (j < P.n) {
-      double s = 0.0;
-      for (int e = P.Psp[j]; e < P.Psp[j + 1]; ++e) s += sb.Ps[P.Psk[e]] * xb[P.Pso[e]];
-      mx = dmaxd(mx, fabs(s * S.Dinv[r]));
-    }
-  }
+  for (int r = 0; r < RN; ++r)
+    if (lane + 64 * r < P.n) mx = dmaxd(mx, fabs(pdx[r] * S.Dinv[r]));
   mx = wave_max(mx);
   if (!(mx < S.c * eps * nrm)) return false;
+  double adx[RM];
+  ell_mv<RM, ELL_KA>(P.eA, sb.vA, xb, adx, lane);
   int bad = 0;
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
-    const int i = lane + 64 * r;
-    if (i < P.m) {
-      double s = 0.0;
-      for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) s += sb.As[P.Ark[q]] * xb[P.Arj[q]];
-      s *= S.Einv[r];
+    if (lane + 64 * r < P.m) {
+      const double s = adx[r] * S.Einv[r];
       if ((S.u[r] < thr && s > eps * nrm) || (S.l[r] > -thr && s < -eps * nrm)) bad = 1;
     }
   }
