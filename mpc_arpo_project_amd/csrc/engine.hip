@@ -56,6 +56,7 @@ struct DevPlan {
   const uint16_t* Lcol;    // DINV slot of each L entry's column
   int inst_doubles;        // LDS doubles of the instance image (16-byte aligned)
   const uint16_t *slotP, *slotA, *slotRho, *slotSig, *wsx, *wsz;
+  const uint16_t *posA, *posP;  // CSC entry -> position in the ELL value copies (symbolic.hpp)
   const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
   int n, m, nk, nnzP, nnzA, nnzL;
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
@@ -404,23 +405,24 @@ struct Inst {
   double Dinv[RN], Einv[RM];  // inverse scalings (termination checks), 1 past the end of x / z
 };
 
-// per-wave scratch slab layout (doubles)
+// per-wave scratch slab layout (doubles): the scalings D, E (unscaling and the infeasibility
+// certificates) and the scaled matrix values in the residual ELL orders (checks, refactorization).
+// 34 KB at N = 20.
 struct Slab {
-  double *Ps, *As, *D, *Dinv, *E, *Einv;
-  double *vA, *vAt, *vP;  // scaled values in the residual ELL orders
+  double *D, *E;
+  double *vA, *vAt, *vP;
 };
+__host__ __device__ __forceinline__ size_t slab_doubles(int n, int m, int eA, int eAt, int eP) {
+  return (size_t)n + m + eA + eAt + eP;
+}
 __device__ __forceinline__ size_t slab_doubles(const DevPlan& P) {
-  return (size_t)P.nnzP + P.nnzA + 2 * P.n + 2 * P.m + P.eA.total + P.eAt.total + P.eP.total;
+  return slab_doubles(P.n, P.m, P.eA.total, P.eAt.total, P.eP.total);
 }
 __device__ __forceinline__ Slab slab_of(const DevPlan& P, double* scr) {
   Slab s;
-  s.Ps = scr;
-  s.As = s.Ps + P.nnzP;
-  s.D = s.As + P.nnzA;
-  s.Dinv = s.D + P.n;
-  s.E = s.Dinv + P.n;
-  s.Einv = s.E + P.m;
-  s.vA = s.Einv + P.m;
+  s.D = scr;
+  s.E = s.D + P.n;
+  s.vA = s.E + P.m;
   s.vAt = s.vA + P.eA.total;
   s.vP = s.vAt + P.eAt.total;
   return s;
@@ -620,10 +622,10 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
   for (int j = lane; j < P.n; j += 64) v[P.slotSig[j]] = p.s.sigma;
   LDS_FENCE();
   for (int k = lane; k < P.nnzP; k += 64) {
-    const double val = sb.Ps[k];
+    const double val = sb.vP[P.posP[k]];
     v[P.slotP[k]] = (P.Pi[k] == P.Pcol[k]) ? val + p.s.sigma : val;
   }
-  for (int k = lane; k < P.nnzA; k += 64) v[P.slotA[k]] = sb.As[k];
+  for (int k = lane; k < P.nnzA; k += 64) v[P.slotA[k]] = sb.vA[P.posA[k]];
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
@@ -978,23 +980,15 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
     S.l[r] = E[r] * S.l[r];
     S.u[r] = E[r] * S.u[r];
     S.Einv[r] = 1. / E[r];
-    if (i < m) {
-      sb.E[i] = E[r];
-      sb.Einv[i] = S.Einv[r];
-    }
+    if (i < m) sb.E[i] = E[r];
   }
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
     S.Dinv[r] = 1. / D[r];
-    if (j < n) {
-      sb.D[j] = D[r];
-      sb.Dinv[j] = S.Dinv[r];
-    }
+    if (j < n) sb.D[j] = D[r];
   }
   // park scaled P, A for residuals / refactorization (per-wave slab)
-  for (int k = lane; k < P.nnzP; k += 64) sb.Ps[k] = v[P.S_P + k];
-  for (int k = lane; k < P.nnzA; k += 64) sb.As[k] = v[P.S_A + k];
   const uint16_t* ix = reinterpret_cast<const uint16_t*>(v) + P.SCI;
   ell_park(P.eA, ix + P.sci_eA, sb.vA, v, lane);
   ell_park(P.eAt, ix + P.sci_eAt, sb.vAt, v, lane);
@@ -1047,12 +1041,12 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const int j = lane + 64 * r;
-      S.x[r] = j < n ? sb.Dinv[j] * p.xs[(size_t)inst * n + j] : 0.0;
+      S.x[r] = j < n ? S.Dinv[r] * p.xs[(size_t)inst * n + j] : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       const int i = lane + 64 * r;
-      S.y[r] = i < m ? (sb.Einv[i] * p.ys[(size_t)inst * m + i]) * S.c : 0.0;
+      S.y[r] = i < m ? (S.Einv[r] * p.ys[(size_t)inst * m + i]) * S.c : 0.0;
     }
     double* xb = v + P.W;
     LDS_FENCE();
@@ -1060,14 +1054,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     for (int r = 0; r < RN; ++r)
       if (lane + 64 * r < n) xb[lane + 64 * r] = S.x[r];
     LDS_FENCE();
+    double az[RM];
+    ell_mv<RM, ELL_KA>(P.eA, sb.vA, xb, az, lane);  // CSR row order
 #pragma unroll
-    for (int r = 0; r < RM; ++r) {
-      const int i = lane + 64 * r;
-      double s = 0.0;
-      if (i < m)
-        for (int q = P.Arp[i]; q < P.Arp[i + 1]; ++q) s += sb.As[P.Ark[q]] * xb[P.Arj[q]];
-      S.z[r] = s;
-    }
+    for (int r = 0; r < RM; ++r) S.z[r] = lane + 64 * r < m ? az[r] : 0.0;
     LDS_FENCE();
   } else {
 #pragma unroll
@@ -1276,7 +1266,8 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     double part = 0.0;
     for (int k = lane; k < P.nnzP; k += 64) {
       const int i = P.Pi[k], j = P.Pcol[k];
-      part += (i == j) ? .5 * sb.Ps[k] * xb[i] * xb[i] : sb.Ps[k] * xb[i] * xb[j];
+      const double pk = sb.vP[P.posP[k]];
+      part += (i == j) ? .5 * pk * xb[i] * xb[i] : pk * xb[i] * xb[j];
     }
 #pragma unroll
     for (int r = 0; r < RN; ++r)
@@ -1531,7 +1522,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
            o_Pso = push_blob(blob, pl.Pso), o_eAs = push_blob(blob, pl.ellA.src),
            o_eAi = push_blob(blob, pl.ellA.in), o_eTs = push_blob(blob, pl.ellAt.src),
            o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
-           o_ePi = push_blob(blob, pl.ellP.in), o_sci = push_blob(blob, pl.sci_block);
+           o_ePi = push_blob(blob, pl.ellP.in), o_sci = push_blob(blob, pl.sci_block),
+           o_pA = push_blob(blob, pl.posA), o_pP = push_blob(blob, pl.posP);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
@@ -1543,6 +1535,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.nfac = pl.nfac, dp.ntail = pl.ntail, dp.nfwd = pl.nfwd, dp.nbwd = pl.nbwd;
     dp.Lcol = (const uint16_t*)(b + o_Lc);
     dp.slotP = (const uint16_t*)(b + o_sP), dp.slotA = (const uint16_t*)(b + o_sA);
+    dp.posA = (const uint16_t*)(b + o_pA), dp.posP = (const uint16_t*)(b + o_pP);
     dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
     dp.wsx = (const uint16_t*)(b + o_wx), dp.wsz = (const uint16_t*)(b + o_wz);
     dp.Ap = (const uint16_t*)(b + o_Ap), dp.Ai = (const uint16_t*)(b + o_Ai);
@@ -1605,9 +1598,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
             (h->dense || hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid *
-                                       ((size_t)pl.nnzP + pl.nnzA + 2 * pl.n + 2 * pl.m +
-                                        pl.ellA.total + pl.ellAt.total + pl.ellP.total)) ==
-                hipSuccess) &&
+                                       slab_doubles(pl.n, pl.m, pl.ellA.total, pl.ellAt.total,
+                                                    pl.ellP.total)) == hipSuccess) &&
             hipMalloc(&h->counter, 64) == hipSuccess;
   if (!ok) return cleanup_fail(MPCQP_E_HIP, "hipMalloc(batch buffers)");
   if (hipMemset(h->has_state, 0, sizeof(int32_t) * Bz) != hipSuccess)

@@ -959,6 +959,21 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     pl.error = "problem too large for the residual layout";
     return false;
   }
+  auto positions = [](const Ell& e, int base, int cnt, std::vector<uint16_t>& pos) {
+    pos.assign(cnt, 0xffff);
+    for (size_t t = 0; t < e.src.size(); ++t) {
+      const int k = (int)e.src[t] - base;
+      if (e.src[t] != 0xffff && k >= 0 && k < cnt && pos[k] == 0xffff) pos[k] = (uint16_t)t;
+    }
+    for (uint16_t x : pos)
+      if (x == 0xffff) return false;
+    return true;
+  };
+  if (!positions(pl.ellA, pl.S_A, pl.nnzA, pl.posA) || !positions(pl.ellP, pl.S_P, pl.nnzP, pl.posP) ||
+      pl.ellA.src.size() >= 65535 || pl.ellP.src.size() >= 65535) {
+    pl.error = "residual layout does not cover every matrix entry";
+    return false;
+  }
   // ---- scaling index overlay behind the scaling value overlay (grows the image only if needed)
   {
     auto& b = pl.sci_block;

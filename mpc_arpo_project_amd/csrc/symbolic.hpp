@@ -121,6 +121,9 @@ struct Plan {
   std::vector<uint16_t> Psp, Psk, Pso; // symmetric traversal: per column j the P entries of
                                        // column j and row j, their position and the other index
   Ell ellA, ellAt, ellP;  // A x (rows of A), A' y (columns), P x (symmetric rows of P)
+  // position of every A entry (CSC order) in ellA's value list and of every P entry (upper CSC) in
+  // ellP's: the per-instance scaled values live only in the ELL copies
+  std::vector<uint16_t> posA, posP;
   int levels_fwd = 0, levels_bwd = 0;
   std::string error;
 };
