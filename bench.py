@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=65536, help="chasers per GPU")
     ap.add_argument("--nx", type=int, default=20)
+    ap.add_argument("--dv", action="store_true", help="impulsive delta-v input model (BASELINE config 3)")
     ap.add_argument("--eps", type=float, default=1e-4)
     ap.add_argument("--seed", type=int, default=20250328)
     ap.add_argument("--cpu-sample", type=int, default=16384)
@@ -125,7 +126,7 @@ def main():
     from mpc_arpo_project_amd import qp_model, scenarios
     from mpc_arpo_project_amd.closed_loop import BatchClosedLoop
 
-    sim, mpc, fail, deb = scenarios.radial_scenario(Nx=args.nx)
+    sim, mpc, fail, deb = scenarios.radial_scenario(Nx=args.nx, isDeltaV=args.dv)
     prob = qp_model.build_problem(sim, mpc, fail, deb)
     B = args.batch
     X0 = initial_states(world * B, rank, B, args.seed)
@@ -203,7 +204,8 @@ def main():
                 "reference test/traj_eval_radial.py)",
         "config": {
             "workload": f"warm closed-loop MPC-QP solves (rescale + LDL' refactor + ADMM), radial "
-                        f"CW scenario, N=Nx={args.nx}, Nc=Nb=5, planar 4-state/2-input model + 5 "
+                        f"CW scenario, N=Nx={args.nx}, Nc=Nb=5, planar 4-state/2-input "
+                        f"{'impulsive delta-v ' if args.dv else ''}model + 5 "
                         f"slacks + 2 disturbances (n={dims['n']}, m={dims['m']}), OSQP 0.6 "
                         f"settings with eps_abs=eps_rel={args.eps:g}",
             "batch_per_gpu": B,
