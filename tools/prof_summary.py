@@ -19,7 +19,8 @@ def main():
     ap.add_argument("--kernel", default="qp_batch_kernel")
     a = ap.parse_args()
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
-    warm = bench["warmup"] if a.warmup is None else a.warmup
+    # the untimed warm-up steps launch the solve kernel once per concurrent shard
+    warm = bench["warmup"] * bench["roofline"].get("concurrent_shards", 1) if a.warmup is None else a.warmup
     rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = np.array([int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]) * 1e-6
