@@ -42,7 +42,8 @@ def main():
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
-    warm = bench["warmup"]
+    S = bench["roofline"].get("concurrent_shards", 1)  # solve launches per step (one per shard)
+    warm = bench["warmup"] * S
 
     cf = np.array(per_dispatch(a.calib_fetch, "calib_read8", "FETCH_SIZE"))
     cw = np.array(per_dispatch(a.calib_write, "calib_write8", "WRITE_SIZE"))
@@ -55,7 +56,11 @@ def main():
     read_b = float(fe.mean()) * f_fetch
     write_b = float(wr.mean()) * f_write
     rl = bench["roofline"]
-    alg = rl["achieved"] * 1e9 * rl["kernel_ms_per_launch"] * 1e-3
+    if S == 1:
+        alg = rl["achieved"] * 1e9 * rl["kernel_ms_per_launch"] * 1e-3
+    else:  # achieved is over the wall time of the timed region; one step = S launches
+        alg = rl["achieved"] * 1e9 * bench["ms_per_step"] * 1e-3 / S
+    per_launch = bench["config"]["batch_per_gpu"] // S
     out = {
         "batch": bench["config"]["batch_per_gpu"],
         "nx": bench["config"]["N"],
@@ -69,8 +74,9 @@ def main():
         "hbm_bytes_per_launch": read_b + write_b,
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": (read_b + write_b) / alg,
-        "solves_per_launch": bench["config"]["batch_per_gpu"],
-        "hbm_bytes_per_solve": (read_b + write_b) / bench["config"]["batch_per_gpu"],
+        "solves_per_launch": per_launch,
+        "concurrent_shards": S,
+        "hbm_bytes_per_solve": (read_b + write_b) / per_launch,
     }
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
