@@ -133,17 +133,15 @@ def main():
     prob = qp_model.build_problem(sim, mpc, fail, deb)
     B = args.batch
     X0 = initial_states(world * B, rank, B, args.seed)
-    S = max(1, args.split)
-    if B % S:
-        raise SystemExit("--batch must be a multiple of --split")
-    Bs = B // S
+    S = max(1, min(args.split, B))
     # S shards of the chasers, each a closed loop on its own HIP stream; shard j holds global chaser
-    # ids [rank*B + j*Bs, ...), so results do not depend on S
+    # ids [rank*B + cut[j], rank*B + cut[j+1]), so results do not depend on S
+    cut = [B * j // S for j in range(S + 1)]
     cls = []
     for j in range(S):
         st_j = torch.cuda.Stream(device=device) if S > 1 else None
-        cls.append(BatchClosedLoop(prob, X0[j * Bs:(j + 1) * Bs], device=device, eps_abs=args.eps,
-                                   eps_rel=args.eps, stream=st_j, id_offset=rank * B + j * Bs))
+        cls.append(BatchClosedLoop(prob, X0[cut[j]:cut[j + 1]], device=device, eps_abs=args.eps,
+                                   eps_rel=args.eps, stream=st_j, id_offset=rank * B + cut[j]))
     torch.cuda.synchronize()
     cl = cls[0]
     dims = cl.qp.dims()
@@ -169,9 +167,9 @@ def main():
             r = c.qp.solve_async()
             ev[j][k][1].record(stream)
             with torch.cuda.stream(stream):
-                iters[k, j * Bs:(j + 1) * Bs].copy_(r.iter, non_blocking=True)
-                rhou[k, j * Bs:(j + 1) * Bs].copy_(r.rho_updates, non_blocking=True)
-                stat[k, j * Bs:(j + 1) * Bs].copy_(r.status, non_blocking=True)
+                iters[k, cut[j]:cut[j + 1]].copy_(r.iter, non_blocking=True)
+                rhou[k, cut[j]:cut[j + 1]].copy_(r.rho_updates, non_blocking=True)
+                stat[k, cut[j]:cut[j + 1]].copy_(r.status, non_blocking=True)
             c.step_after_solve(r)
     torch.cuda.synchronize()
     if dist:
