@@ -52,3 +52,23 @@ def test_shard_invariance(prob20):
     assert torch.equal(rf.iter[16:32], rp.iter)
     full.close()
     part.close()
+
+
+def test_sharded_closed_loop_matches_single_stream(prob20):
+    """two shards on concurrent streams reproduce the one-stream batch bit for bit"""
+    from mpc_arpo_project_amd.closed_loop import ShardedClosedLoop
+
+    X = scenarios.sample_estimates(40, seed=11)[:, :4]
+    X[:, 2:] = 0.0
+    one = BatchClosedLoop(prob20, X, eps_abs=1e-4, eps_rel=1e-4)
+    two = ShardedClosedLoop(prob20, X, shards=2, eps_abs=1e-4, eps_rel=1e-4)
+    for _ in range(6):
+        r1 = one.step()
+        r2 = two.step()
+    two.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(one.x_true, two.x_true)
+    assert torch.equal(r1.iter, torch.cat([r.iter for r in r2]))
+    assert torch.equal(one.ctrl_seq, two.ctrl_seq)
+    one.close()
+    two.close()
