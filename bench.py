@@ -195,6 +195,10 @@ def main():
         achieved = float(np.mean(per_solve.sum(axis=1) / kt[0])) / 1e9
     else:  # overlapping launches: all algorithmic bytes over the wall time of the timed region
         achieved = float(per_solve.sum() / elapsed) / 1e9
+    # the per-launch form (a shard's step bytes over that launch's own duration), which undercounts
+    # when launches overlap: reported beside `achieved` for transparency
+    shard_bytes = np.stack([per_solve[:, cut[j]:cut[j + 1]].sum(axis=1) for j in range(S)])  # (S, K)
+    achieved_per_launch = float(np.mean(shard_bytes / kt)) / 1e9
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -242,6 +246,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
+            "achieved_per_launch": achieved_per_launch,
             "traffic": traffic,
             "kernel": "qp_batch_kernel",
             "kernel_ms_per_launch": float(np.mean(kt) * 1e3),
