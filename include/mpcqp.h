@@ -56,7 +56,6 @@ extern "C" {
 
 /* linear-system engines (mpcqp_engine_kind) */
 #define MPCQP_ENGINE_KKT 0    /* blocked level-scheduled LDL' of the quasi-definite KKT matrix */
-#define MPCQP_ENGINE_DENSE 1  /* explicit inverse of P + sigma I + A' diag(rho) A (n <= 128) */
 
 /* OSQP 0.6 status_val values */
 #define MPCQP_SOLVED 1
@@ -133,6 +132,19 @@ int mpcqp_data_buffers(mpcqp_handle *h, double **Ax, double **l, double **u);
  * Ax [B*nnzA], l, u [B*m]. */
 int mpcqp_copy_data(mpcqp_handle *h, double *Ax, double *l, double *u);
 
+/* Register a skip mask (device [B] int32, read by every following mpcqp_solve; NULL clears it):
+ * instances with skip[i] != 0 are not solved and keep their outputs and warm state.  A batch of
+ * closed loops passes its `done` flags, so chasers whose run has terminated cost nothing (the
+ * reference stops calling solve() at termination, src/trajectorySimulate.py:288-296). */
+int mpcqp_set_skip(mpcqp_handle *h, const int32_t *skip);
+
+/* Copy the warm-start state the handle carries between solves (what OSQP keeps inside its
+ * workspace) into caller device buffers (any may be NULL): the SCALED iterates xs [B*n], zs, ys
+ * [B*m], rho [B] and has_state [B] (0: never solved / reset, 1: iterates of the last solve).
+ * For white-box parity tests (the oracle's oqp_get_state counterpart). */
+int mpcqp_get_state(const mpcqp_handle *h, double *xs, double *zs, double *ys, double *rho,
+                    int32_t *has_state);
+
 /* Introspection. */
 int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA,
                int32_t *nnzL);
@@ -140,9 +152,8 @@ int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int
  * triangular solves, LDS bytes per instance and resident waves (instances in flight) per CU. */
 int mpcqp_schedule_info(const mpcqp_handle *h, int32_t *fac_steps, int32_t *fwd_steps,
                         int32_t *bwd_steps, int32_t *lds_bytes, int32_t *waves_per_cu);
-/* Which linear-system engine the handle runs: the dense-inverse engine is chosen for n <= 128 and
- * m <= 256, the KKT engine otherwise; environment variable MPCQP_ENGINE=kkt|dense (read by
- * mpcqp_create) forces one.  Both give OSQP 0.6's iterates up to rounding. */
+/* Which linear-system engine the handle runs (MPCQP_ENGINE_KKT: the only engine of this build;
+ * round 1's dense-inverse alternative measured slower and was removed). */
 int mpcqp_engine_kind(const mpcqp_handle *h, int32_t *kind);
 /* Host-only symbolic analysis (no HIP call; usable without a GPU): KKT ordering, L pattern and
  * schedule statistics for a structure.  perm [n+m], Lp [n+m+1] may be NULL; Li is written only

@@ -69,6 +69,18 @@ int mpcqp_cl_step(mpcqp_cl *cl, const int32_t *status, const double *x_sol, int3
                   double *xest, int32_t *done, int32_t *ctrl_seq, double *ctrl_out,
                   const double *noise, double *z, double *u_applied);
 
+/* Per-chaser run summary kept up to date by every following mpcqp_cl_step (device buffers [B],
+ * all four or none; NULL disables; the caller initialises them: iterm = nsim (or 0 for chasers
+ * terminated at x0), success = 0, final_err = 0, n_fallback = 0):
+ *   iterm      loop index at which the termination test fired (src/trajectorySimulate.py:288-293)
+ *   success    1 once a state x(i), 1 <= i < iterm, is within dist_tol of xr with approach angle
+ *              |atan(vy / vx)| <= ang_tol degrees (the reference's success test, :369-376)
+ *   final_err  |x(iterm - 1) - xr|_2 (test/disturbRejComp.py:88), or of the last state stepped
+ *   n_fallback steps that used the failsafe / deadbeat controller instead of the MPC solution
+ * The step index counts mpcqp_cl_step calls on this handle. */
+int mpcqp_cl_set_tracking(mpcqp_cl *cl, int32_t *iterm, int32_t *success, double *final_err,
+                          int32_t *n_fallback, double dist_tol, double ang_tol);
+
 /* Global id of instance 0 of this handle (a rank's shard offset); keys the noise streams. */
 int mpcqp_cl_set_ids(mpcqp_cl *cl, int64_t id0);
 

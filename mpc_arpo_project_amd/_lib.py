@@ -18,10 +18,10 @@ LIB_PATH = os.environ.get("MPCQP_LIBRARY") or os.path.join(_HERE, "libmpcqp.so")
 EXPORTED = (
     "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",
     "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
-    "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
+    "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_get_state", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
     "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind",
     "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
-    "mpcqp_cl_set_ids", "mpcqp_cl_noise", "mpcqp_cl_set_plant", "mpcqp_clc_period",
+    "mpcqp_cl_set_ids", "mpcqp_cl_set_tracking", "mpcqp_cl_noise", "mpcqp_cl_set_plant", "mpcqp_clc_period",
     "mpcqp_ukf_create", "mpcqp_ukf_destroy", "mpcqp_ukf_step", "mpcqp_plant_rk45",
 )
 
@@ -115,6 +115,8 @@ def lib():
     L.mpcqp_dims.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
     L.mpcqp_engine_kind.argtypes = [vp, i32p]
     L.mpcqp_copy_data.argtypes = [vp, dp, dp, dp]
+    L.mpcqp_get_state.argtypes = [vp, dp, dp, dp, dp, dp]
+    L.mpcqp_set_skip.argtypes = [vp, dp]
     L.mpcqp_data_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
     L.mpcqp_schedule_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
     L.mpcqp_export_symbolic.argtypes = [vp, i32p, i32p, i32p]
@@ -124,6 +126,7 @@ def lib():
     L.mpcqp_cl_configure.argtypes = [vp, dp, dp, dp, dp]
     L.mpcqp_cl_step.argtypes = [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]
     L.mpcqp_cl_set_ids.argtypes = [vp, C.c_int64]
+    L.mpcqp_cl_set_tracking.argtypes = [vp, dp, dp, dp, dp, C.c_double, C.c_double]
     L.mpcqp_cl_noise.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_double, C.c_double, dp]
     L.mpcqp_cl_set_plant.argtypes = [vp, C.POINTER(PlantModel), i32]
     L.mpcqp_clc_period.argtypes = [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp,

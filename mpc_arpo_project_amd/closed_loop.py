@@ -123,6 +123,8 @@ class BatchClosedLoop:
             raise MPCQPError(f"mpcqp_cl_create failed ({rc})")
         self._cl = h
         self._bufs = data_buffers(self.qp)
+        # terminated chasers are not solved again (the reference leaves its loop at termination)
+        self.qp.set_skip(self.done)
         self.u0 = prob.u0_slice.start
         self.steps = 0
         check(_lib.lib().mpcqp_cl_set_ids(self._cl, int(id_offset)), "mpcqp_cl_set_ids")
@@ -169,9 +171,56 @@ class BatchClosedLoop:
         """Solve the current QPs, apply the controller and plant, rebuild the QP data (async)."""
         return self.step_after_solve(self.qp.solve_async())
 
+    def enable_tracking(self, nsim, dist_tol=0.2, ang_tol=45.0):
+        """Keep the per-chaser run summary on the device from now on (call before the first step):
+        the reference's run reduction -- i_term, isSuccess (src/trajectorySimulate.py:288-293,
+        369-376), the final error |x(i_term - 1) - xr| of test/disturbRejComp.py:88 -- plus the
+        first MPC input, the last solve status, total ADMM iterations and fallback-step count.
+        `summary()` packs them."""
+        if self.steps:
+            raise MPCQPError("enable_tracking must precede the first step")
+        i32 = dict(dtype=torch.int32, device=self.device)
+        self.iterm = torch.where(self.done > 0, 0, int(nsim)).to(torch.int32).contiguous()
+        self.success = torch.zeros(self.B, **i32)
+        self.n_fallback = torch.zeros(self.B, **i32)
+        self.final_err = torch.zeros(self.B, dtype=torch.float64, device=self.device)
+        self.iters_total = torch.zeros(self.B, dtype=torch.int64, device=self.device)
+        self.last_status = torch.zeros(self.B, **i32)
+        self.u0_first = torch.full((self.B, 2), float("nan"), dtype=torch.float64,
+                                   device=self.device)
+        check(_lib.lib().mpcqp_cl_set_tracking(self._cl, self.iterm.data_ptr(),
+                                               self.success.data_ptr(), self.final_err.data_ptr(),
+                                               self.n_fallback.data_ptr(), float(dist_tol),
+                                               float(ang_tol)), "mpcqp_cl_set_tracking")
+        self._tracking = True
+
+    SUMMARY_FIELDS = ("u0_x", "u0_y", "last_status", "admm_iters", "i_term", "success",
+                      "final_err", "n_fallback")
+
+    def summary(self):
+        """(B, 8) float64 device tensor, columns SUMMARY_FIELDS (ordered after this loop's stream)"""
+        if not getattr(self, "_tracking", False):
+            raise MPCQPError("enable_tracking() first")
+        torch.cuda.current_stream(self.device).wait_stream(self.qp.stream)
+        return torch.cat([self.u0_first, self.last_status[:, None].double(),
+                          self.iters_total[:, None].double(), self.iterm[:, None].double(),
+                          self.success[:, None].double(), self.final_err[:, None],
+                          self.n_fallback[:, None].double()], dim=1)
+
+    def _track_solve(self, r):
+        with torch.cuda.stream(self.qp.stream):
+            active = self.done == 0
+            self.iters_total += torch.where(active, r.iter, 0).to(torch.int64)
+            self.last_status.copy_(torch.where(active, r.status, self.last_status))
+            if self.steps == 0:
+                u = r.x[:, self.u0:self.u0 + 2]
+                self.u0_first.copy_(torch.where(active[:, None], u, self.u0_first))
+
     def step_after_solve(self, r):
         """Controller select + plant + QP-data rebuild for a solve already enqueued (async)."""
         L = _lib.lib()
+        if getattr(self, "_tracking", False):
+            self._track_solve(r)
         opt = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         rc = L.mpcqp_cl_step(self._cl, r.status.data_ptr(), r.x.data_ptr(), self.qp.n, self.u0,
                              self.x_true.data_ptr(), self.ctrl_prev.data_ptr(),
@@ -216,17 +265,35 @@ class ShardedClosedLoop:
     the unsharded loop: chasers are independent and keep their global ids (noise streams).
     """
 
-    def __init__(self, prob: MPCProblem, x0, shards=2, device="cuda", id_offset=0, **kw):
+    def __init__(self, prob: MPCProblem, x0, shards=2, device="cuda", id_offset=0,
+                 noise_source=None, **kw):
         x0 = np.asarray(x0, dtype=float)
         B = x0.shape[0]
         S = max(1, min(int(shards), B))
         self.cut = [B * j // S for j in range(S + 1)]
         dev = torch.device(device)
         self.parts = []
+        # a host noise source draws for the WHOLE batch (e.g. numpy's seeded global generator):
+        # draw k once, cache it, hand each shard its rows, so the host RNG advances exactly as in
+        # the unsharded loop
+        self._draw_k, self._draw_w = None, None
+
+        def shard_source(j):
+            if noise_source is None:
+                return None
+
+            def draw(k, a=self.cut[j], b=self.cut[j + 1]):
+                if self._draw_k != k:
+                    self._draw_w = np.asarray(noise_source(k), dtype=float).reshape(B, 4)
+                    self._draw_k = k
+                return self._draw_w[a:b]
+            return draw
+
         for j in range(S):
             st = torch.cuda.Stream(device=dev) if S > 1 else None
             self.parts.append(BatchClosedLoop(prob, x0[self.cut[j]:self.cut[j + 1]], device=dev,
-                                              id_offset=id_offset + self.cut[j], stream=st, **kw))
+                                              id_offset=id_offset + self.cut[j], stream=st,
+                                              noise_source=shard_source(j), **kw))
         torch.cuda.synchronize(dev)
 
     def step(self):
@@ -234,7 +301,20 @@ class ShardedClosedLoop:
         return [c.step() for c in self.parts]
 
     def _cat(self, name):
+        # each shard writes its buffers on its own stream: order the caller's stream after them
+        cur = torch.cuda.current_stream(self.parts[0].device)
+        for c in self.parts:
+            cur.wait_stream(c.qp.stream)
         return torch.cat([getattr(c, name) for c in self.parts])
+
+    def enable_tracking(self, nsim, dist_tol=0.2, ang_tol=45.0):
+        for c in self.parts:
+            c.enable_tracking(nsim, dist_tol, ang_tol)
+
+    SUMMARY_FIELDS = BatchClosedLoop.SUMMARY_FIELDS
+
+    def summary(self):
+        return torch.cat([c.summary() for c in self.parts])
 
     @property
     def x_true(self):

@@ -22,10 +22,18 @@ using mpcqp::rk45_interval;
 
 constexpr int NX = 4, NU = 2, NY = 5, NDI = 2;
 
+// per-chaser run summary (mpcqp_cl_set_tracking), updated by cl_step_kernel
+struct Track {
+  int32_t *iterm, *success, *n_fallback;
+  double* final_err;
+  double dist_tol, ang_tol, rad2deg;
+  int32_t step;  // loop index i of the step being launched: x_true holds x(i)
+};
 struct ClDev {
   mpcqp_cl_scenario sc;  // host pointers inside are not used on the device
   const int32_t *pos_c1, *pos_c2, *pos_slope;
   int B;
+  Track tr;
 };
 
 __device__ __forceinline__ double mul(double a, double b) { return __dmul_rn(a, b); }
@@ -182,6 +190,23 @@ __global__ void __launch_bounds__(256) cl_step_kernel(ClDev d, const int32_t* st
   const int seq = select_control(s, status[b], x_sol + (size_t)b * n + u0, xe, xi, c0, c1);
   xintf[b] = xi;
   ctrl_seq[b] = seq;
+  const Track& tr = d.tr;
+  if (tr.iterm) {
+    // the reference's run reduction (src/trajectorySimulate.py:369-376 success test over the
+    // states 1 .. iterm-1 of the run; test/disturbRejComp.py:88 final error |x(iterm-1) - xr|)
+    const double* x = x_true + (size_t)b * NX;
+    const double e0 = sub(x[0], s.xr[0]), e1 = sub(x[1], s.xr[1]);
+    const double dist = sqrt(add(mul(e0, e0), mul(e1, e1)));
+    const double ang = mul(fabs(atan(x[3] / x[2])), tr.rad2deg);
+    if (tr.step >= 1 && dist <= tr.dist_tol && ang <= tr.ang_tol) tr.success[b] = 1;
+    double e2 = 0.0;
+    for (int k = 0; k < NX; ++k) {
+      const double ek = sub(x[k], s.xr[k]);
+      e2 = add(e2, mul(ek, ek));
+    }
+    tr.final_err[b] = sqrt(e2);
+    if (seq != 1) tr.n_fallback[b] += 1;
+  }
   ctrl_out[(size_t)b * 2] = c0;
   ctrl_out[(size_t)b * 2 + 1] = c1;
   // plant in CSC column order (scipy sparse mat-vec), then + noise
@@ -209,7 +234,10 @@ __global__ void __launch_bounds__(256) cl_step_kernel(ClDev d, const int32_t* st
   xw[4] = 0.0;
   xw[5] = 0.0;
   if (z_out) measure(xn, z_out + (size_t)b * 2);
-  if (terminated(s, xn)) done[b] = 1;
+  if (terminated(s, xn)) {
+    done[b] = 1;
+    if (tr.iterm) tr.iterm[b] = tr.step + 1;
+  }
 }
 
 // Philox-4x32-10 (Salmon et al., SC'11): counter (draw, id) under key (seed)
@@ -277,6 +305,23 @@ __global__ void __launch_bounds__(64) clc_period_kernel(
   const int seq = select_control(s, status[b], x_sol + (size_t)b * n + u0, xe, xi, c0, c1);
   xintf[b] = xi;
   ctrl_seq[b] = seq;
+  const Track& tr = d.tr;
+  if (tr.iterm) {
+    // the reference's run reduction (src/trajectorySimulate.py:369-376 success test over the
+    // states 1 .. iterm-1 of the run; test/disturbRejComp.py:88 final error |x(iterm-1) - xr|)
+    const double* x = x_true + (size_t)b * NX;
+    const double e0 = sub(x[0], s.xr[0]), e1 = sub(x[1], s.xr[1]);
+    const double dist = sqrt(add(mul(e0, e0), mul(e1, e1)));
+    const double ang = mul(fabs(atan(x[3] / x[2])), tr.rad2deg);
+    if (tr.step >= 1 && dist <= tr.dist_tol && ang <= tr.ang_tol) tr.success[b] = 1;
+    double e2 = 0.0;
+    for (int k = 0; k < NX; ++k) {
+      const double ek = sub(x[k], s.xr[k]);
+      e2 = add(e2, mul(ek, ek));
+    }
+    tr.final_err[b] = sqrt(e2);
+    if (seq != 1) tr.n_fallback[b] += 1;
+  }
   ctrl_out[(size_t)b * 2] = c0;
   ctrl_out[(size_t)b * 2 + 1] = c1;
   double* up = ctrl_prev + (size_t)b * NU;
@@ -339,6 +384,7 @@ struct mpcqp_cl {
   bool has_plant = false;   // continuous-time plant set (mpcqp_cl_set_plant)
   PlantConsts pc{};
   int isDeltaV = 0;
+  int32_t steps = 0;  // mpcqp_cl_step calls so far (the loop index of the next step)
 };
 
 extern "C" {
@@ -395,10 +441,23 @@ int mpcqp_cl_step(mpcqp_cl* cl, const int32_t* status, const double* x_sol, int3
       !ctrl_seq || !ctrl_out)
     return -1;
   const int B = cl->d.B;
+  cl->d.tr.step = cl->steps++;
   hipLaunchKernelGGL(cl_step_kernel, dim3((B + 255) / 256), dim3(256), 0, cl->stream, cl->d,
                      status, x_sol, n, u0_offset, x_true, ctrl_prev, xintf, xest, done, ctrl_seq,
                      ctrl_out, noise, z, u_applied);
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int mpcqp_cl_set_tracking(mpcqp_cl* cl, int32_t* iterm, int32_t* success, double* final_err,
+                          int32_t* n_fallback, double dist_tol, double ang_tol) {
+  if (!cl) return -1;
+  const bool any = iterm || success || final_err || n_fallback;
+  if (any && !(iterm && success && final_err && n_fallback)) return -1;
+  Track& t = cl->d.tr;
+  t.iterm = iterm, t.success = success, t.final_err = final_err, t.n_fallback = n_fallback;
+  t.dist_tol = dist_tol, t.ang_tol = ang_tol;
+  t.rad2deg = 180.0 / 3.141592653589793;  // the reference's (180/np.pi)
+  return 0;
 }
 
 int mpcqp_cl_set_ids(mpcqp_cl* cl, int64_t id0) {

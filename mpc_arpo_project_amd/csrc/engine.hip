@@ -26,8 +26,6 @@
 
 #include "../../include/mpcqp.h"
 #include "symbolic.hpp"
-#include "dense.hpp"
-#include "dense_dev.hpp"
 
 using namespace mpcqp;
 
@@ -84,6 +82,7 @@ struct KParams {
   // read per instance from the kernel arguments instead of a loop-invariant register (the gfx950
   // backend of ROCm 7.2 was seen to spill such a hoisted double and reload only its low half)
   double rho0;
+  const int32_t* skip;  // [B] or null: instances with skip[i] != 0 are not solved (outputs kept)
 };
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
@@ -1329,6 +1328,7 @@ __global__ void __launch_bounds__(64) qp_batch_kernel(KParams p) {
     inst = (unsigned int)__shfl((int)inst, 0);
     inst = __builtin_amdgcn_readfirstlane(inst);
     if (inst >= (unsigned int)p.B) break;
+    if (p.skip && p.skip[inst]) continue;  // wave-uniform
     solve_instance<RN, RM>(p, (int)inst, v, scr, lane);
     LDS_FENCE();
   }
@@ -1396,8 +1396,8 @@ struct mpcqp_handle {
   double* scratch = nullptr;
   unsigned int* counter = nullptr;
   unsigned long long* timing = nullptr;  // MPCQP_TIMING builds
-  DenseEngine* dense = nullptr;          // dense-inverse engine (dense.hip) when selected
   bool has_data = false;
+  const int32_t* skip = nullptr;  // mpcqp_set_skip
   int grid = 0, lds_bytes = 0, waves_per_cu = 0;
   kernel_fn kern = nullptr;
 };
@@ -1472,36 +1472,11 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, "internal: empty schedule");
   }
-  // engine: the KKT engine by default; MPCQP_ENGINE=dense selects the dense-inverse engine for
-  // small problems (dense.hpp).  Measured on the bench workload the dense engine is
-  // slower (one instance per CU) and its explicit inverse less exact on infeasible instances,
-  // so it is opt-in.
-  const char* eng = getenv("MPCQP_ENGINE");
-  const bool force_dense = eng && strcmp(eng, "dense") == 0;
-  if (force_dense && !dense_supported(pl.n, pl.m)) {
-    delete h;
-    return fail(MPCQP_E_UNSUPPORTED, "MPCQP_ENGINE=dense: n <= 128 and m <= 256 required");
-  }
-  if (force_dense) {
-    DenseInputs di{st->n, st->m, batch, st->Pp, st->Pi, st->Ap, st->Ai};
-    std::string err;
-    const int rc = dense_create(di, &h->dense, err);
-    if (rc != 0 && (force_dense || rc != MPCQP_E_UNSUPPORTED)) {
-      delete h;
-      return fail(rc, err);
-    }
-    if (rc != 0 && getenv("MPCQP_DEBUG"))
-      fprintf(stderr, "mpcqp: dense engine not used (%s); KKT engine\n", err.c_str());
-    if (h->dense) {  // (a structure the dense engine cannot lay out falls back to the KKT engine)
-      dense_info(h->dense, &h->grid, &h->lds_bytes, &h->waves_per_cu);
-      h->waves_per_cu *= DENSE_THREADS / 64;
-    }
-  }
   auto cleanup_fail = [&](int code, const std::string& msg) {
     mpcqp_destroy(h);
     return fail(code, msg);
   };
-  if (!h->dense) {
+  {
     h->kern = select_kernel(pl.n, pl.m);
     if (!h->kern) {
       delete h;
@@ -1572,17 +1547,19 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
       return cleanup_fail(MPCQP_E_HIP, "hipDeviceGetAttribute");
     const int inst_bytes = dp.inst_doubles * 8;
     const int lds_cap = 160 * 1024;
-    if (inst_bytes > lds_cap)
+    // diagnostic: MPCQP_LDS_PAD extra bytes per workgroup (occupancy scans; never set in product)
+    const int lds_alloc = inst_bytes + std::max(0, env_int("MPCQP_LDS_PAD", 0));
+    if (lds_alloc > lds_cap)
       return cleanup_fail(MPCQP_E_UNSUPPORTED, "instance image exceeds the LDS of a CU");
     if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             lds_cap) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipFuncSetAttribute");
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, 64, inst_bytes) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, 64, lds_alloc) !=
             hipSuccess || nb <= 0)
       return cleanup_fail(MPCQP_E_UNSUPPORTED, "kernel does not fit on a CU (LDS/VGPR)");
     h->waves_per_cu = nb;
-    h->lds_bytes = inst_bytes;
+    h->lds_bytes = lds_alloc;
     h->grid = std::min(batch, nb * ncu);
   }
   const size_t Bz = (size_t)batch;
@@ -1597,9 +1574,9 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->Ecls, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
-            (h->dense || hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid *
+            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid *
                                        slab_doubles(pl.n, pl.m, pl.ellA.total, pl.ellAt.total,
-                                                    pl.ellP.total)) == hipSuccess) &&
+                                                    pl.ellP.total)) == hipSuccess &&
             hipMalloc(&h->counter, 64) == hipSuccess;
   if (!ok) return cleanup_fail(MPCQP_E_HIP, "hipMalloc(batch buffers)");
   if (hipMemset(h->has_state, 0, sizeof(int32_t) * Bz) != hipSuccess)
@@ -1610,7 +1587,6 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
 
 int mpcqp_destroy(mpcqp_handle* h) {
   if (!h) return 0;
-  dense_destroy(h->dense);
   void* bufs[] = {h->d_blob, h->Px, h->q,    h->Ax,        h->l,       h->u,      h->xs,
                   h->zs,     h->ys, h->Ecls, h->rho, h->has_state, h->scratch, h->counter};
   for (void* b : bufs)
@@ -1689,20 +1665,8 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   p.counter = h->counter;
   p.timing = h->timing;
   p.rho0 = std::min(std::max(h->set.rho, RHO_MIN), RHO_MAX);
+  p.skip = h->skip;
   HIPCHK(hipMemsetAsync(h->counter, 0, 64, h->stream));
-  if (h->dense) {
-    DenseSolveArgs a{};
-    a.s = h->set, a.B = h->B;
-    a.Px = h->Px, a.q = h->q, a.Ax = h->Ax, a.l = h->l, a.u = h->u;
-    a.xs = h->xs, a.zs = h->zs, a.ys = h->ys, a.rho_state = h->rho, a.Ecls = h->Ecls;
-    a.has_state = h->has_state, a.x_out = x, a.y_out = y;
-    if (info) a.info = *info;
-    a.counter = h->counter;
-    a.timing = h->timing;
-    if (dense_solve(h->dense, a, h->stream) != 0)
-      return fail(MPCQP_E_HIP, std::string("dense kernel launch: ") + hipGetErrorString(hipGetLastError()));
-    return 0;
-  }
   hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(64), h->lds_bytes, h->stream, p);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1740,6 +1704,27 @@ int mpcqp_copy_data(mpcqp_handle* h, double* Ax, double* l, double* u) {
   return 0;
 }
 
+int mpcqp_set_skip(mpcqp_handle* h, const int32_t* skip) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  h->skip = skip;
+  return 0;
+}
+
+int mpcqp_get_state(const mpcqp_handle* h, double* xs, double* zs, double* ys, double* rho,
+                    int32_t* has_state) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  const size_t B = (size_t)h->B;
+  const Plan& pl = h->plan;
+  if (xs) HIPCHK(hipMemcpyAsync(xs, h->xs, sizeof(double) * B * pl.n, hipMemcpyDeviceToDevice, h->stream));
+  if (zs) HIPCHK(hipMemcpyAsync(zs, h->zs, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
+  if (ys) HIPCHK(hipMemcpyAsync(ys, h->ys, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
+  if (rho) HIPCHK(hipMemcpyAsync(rho, h->rho, sizeof(double) * B, hipMemcpyDeviceToDevice, h->stream));
+  if (has_state)
+    HIPCHK(hipMemcpyAsync(has_state, h->has_state, sizeof(int32_t) * B, hipMemcpyDeviceToDevice,
+                          h->stream));
+  return 0;
+}
+
 int mpcqp_dims(const mpcqp_handle* h, int32_t* n, int32_t* m, int32_t* nnzP, int32_t* nnzA,
                int32_t* nnzL) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");
@@ -1754,9 +1739,9 @@ int mpcqp_dims(const mpcqp_handle* h, int32_t* n, int32_t* m, int32_t* nnzP, int
 int mpcqp_schedule_info(const mpcqp_handle* h, int32_t* fac, int32_t* fwd, int32_t* bwd,
                         int32_t* lds, int32_t* wpc) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");
-  if (fac) *fac = h->dense ? 0 : (int32_t)(h->plan.nfac + h->plan.ntail);
-  if (fwd) *fwd = h->dense ? 0 : (int32_t)h->plan.nfwd;
-  if (bwd) *bwd = h->dense ? 0 : (int32_t)h->plan.nbwd;
+  if (fac) *fac = (int32_t)(h->plan.nfac + h->plan.ntail);
+  if (fwd) *fwd = (int32_t)h->plan.nfwd;
+  if (bwd) *bwd = (int32_t)h->plan.nbwd;
   if (lds) *lds = h->lds_bytes;
   if (wpc) *wpc = h->waves_per_cu;
   return 0;
@@ -1764,7 +1749,7 @@ int mpcqp_schedule_info(const mpcqp_handle* h, int32_t* fac, int32_t* fwd, int32
 
 int mpcqp_engine_kind(const mpcqp_handle* h, int32_t* kind) {
   if (!h || !kind) return fail(MPCQP_E_INVALID, "null argument");
-  *kind = h->dense ? MPCQP_ENGINE_DENSE : MPCQP_ENGINE_KKT;
+  *kind = MPCQP_ENGINE_KKT;
   return 0;
 }
 

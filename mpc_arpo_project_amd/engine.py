@@ -160,6 +160,30 @@ class BatchQP:
               "mpcqp_copy_data")
         return Ax, l, u
 
+    def set_skip(self, mask):
+        """int32 device tensor [B] (kept alive by the handle) or None: instances with a non-zero
+        entry are skipped by every following solve (outputs and warm state unchanged)"""
+        if mask is not None:
+            if mask.dtype != torch.int32 or tuple(mask.shape) != (self.B,) or \
+                    mask.device != self.device or not mask.is_contiguous():
+                raise ValueError(f"skip mask must be a contiguous int32 tensor of shape ({self.B},)")
+        check(_lib.lib().mpcqp_set_skip(self._h, None if mask is None else mask.data_ptr()),
+              "mpcqp_set_skip")
+        self._skip = mask
+
+    def get_state(self):
+        """Warm-start state carried to the next solve (scaled xs, zs, ys; rho; has_state), as new
+        device tensors -- the white-box hook the oracle's `state()` mirrors."""
+        f = dict(dtype=torch.float64, device=self.device)
+        xs = torch.empty(self.B, self.n, **f)
+        zs = torch.empty(self.B, self.m, **f)
+        ys = torch.empty(self.B, self.m, **f)
+        rho = torch.empty(self.B, **f)
+        hs = torch.empty(self.B, dtype=torch.int32, device=self.device)
+        check(_lib.lib().mpcqp_get_state(self._h, xs.data_ptr(), zs.data_ptr(), ys.data_ptr(),
+                                         rho.data_ptr(), hs.data_ptr()), "mpcqp_get_state")
+        return dict(x=xs, z=zs, y=ys, rho=rho, has_state=hs)
+
     def warm_start(self, x, y):
         x = self._batch_vec(x, self.n, "x")
         y = self._batch_vec(y, self.m, "y")
@@ -200,7 +224,7 @@ class BatchQP:
               "mpcqp_schedule_info")
         k = C.c_int32()
         check(_lib.lib().mpcqp_engine_kind(self._h, C.byref(k)), "mpcqp_engine_kind")
-        return dict(engine="dense" if k.value == 1 else "kkt", fac_steps=v[0].value,
+        return dict(engine="kkt", fac_steps=v[0].value,
                     fwd_steps=v[1].value, bwd_steps=v[2].value, lds_bytes=v[3].value,
                     waves_per_cu=v[4].value)
 

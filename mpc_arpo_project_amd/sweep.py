@@ -1,0 +1,213 @@
+"""Monte-Carlo sweeps of the closed loop over (noise seed x initial condition) -- BASELINE config 5.
+
+The reference runs its experiments as serial Python loops of `trajectorySimulate`:
+  * test/saved_runs/success_rates_test.py:64-75   MCnum runs, counting `isSuccess`;
+  * test/disturbRejComp.py:77-100                  noise lengths x MC runs, final distance
+                                                   |x(i_term - 1) - xr| with / without rejection;
+  * test/traj_eval_radial.py, traj_eval_in_track.py  the two approach geometries.
+(Every one of those runs re-seeds numpy with 123 at the top of trajectorySimulate,
+src/trajectorySimulate.py:28, so the reference's "Monte-Carlo" repetitions are identical runs;
+a sweep here gives every scenario its own noise stream instead.)
+
+A sweep is G = n_seeds x n_ics independent chasers; scenario g = s * n_ics + c runs initial
+condition c under noise stream g:
+  * initial conditions: seeded samples inside the approach's line-of-sight cone, at rest
+    (`initial_conditions`);
+  * noise (when given): the device's counter-based Philox stream keyed by (noise_seed, g, draw),
+    so a scenario's result does not depend on how the sweep is sharded;
+  * one process per GPU; rank r owns the contiguous ids [r G / W, (r + 1) G / W), split into
+    `shards` closed loops on concurrent HIP streams; terminated chasers are skipped by the solver;
+  * the only collective: after the run, one all-gather (RCCL over xGMI) of the per-scenario
+    summary (8 float64: first MPC input, last status, ADMM iterations, i_term, success,
+    final error, fallback steps); optionally the trajectories are gathered to rank 0.
+
+    python -m mpc_arpo_project_amd.sweep --scenario radial --seeds 1024 --ics 1024 --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+
+import numpy as np
+
+from . import launch, scenarios
+
+FIELDS = ("u0_x", "u0_y", "last_status", "admm_iters", "i_term", "success", "final_err",
+          "n_fallback")
+
+
+def initial_conditions(scenario: str, n_ics: int, seed: int = 20250328) -> np.ndarray:
+    """(n_ics, 4) chaser states at rest inside the LOS cone: the radial approach samples
+    x in [20, 110] m, |y| <= 15 m (scenarios.sample_estimates); the in-track approach is the
+    same geometry turned on its side (x and y swapped, approach along +y)."""
+    X = scenarios.sample_estimates(n_ics, seed=seed)[:, :4].copy()
+    X[:, 2:4] = 0.0
+    if scenario == "in_track":
+        X[:, [0, 1]] = X[:, [1, 0]]
+    elif scenario != "radial":
+        raise ValueError(f"unknown scenario {scenario!r}")
+    return X
+
+
+def scenario_states(scenario: str, n_seeds: int, n_ics: int, lo: int, hi: int, ic_seed: int):
+    """initial states of global scenario ids [lo, hi) (g = s * n_ics + c -> IC c)"""
+    ics = initial_conditions(scenario, n_ics, ic_seed)
+    g = np.arange(lo, hi)
+    assert hi <= n_seeds * n_ics
+    return ics[g % n_ics]
+
+
+def build(scenario: str, Nx: int, noise, isReject: bool, T_final: float):
+    from . import qp_model
+    from .mpcsim import Noise
+
+    nz = None if noise is None else Noise((noise[0], noise[1]), noise[2])
+    if scenario == "radial":
+        sim, mpc, fail, deb = scenarios.radial_scenario(Nx=Nx, isReject=isReject, noise=nz,
+                                                        T_final=T_final)
+    else:
+        sim, mpc, fail, deb = scenarios.in_track_scenario(Nx=Nx, isReject=isReject, noise=nz,
+                                                          T_final=T_final)
+    return sim, qp_model.build_problem(sim, mpc, fail, deb)
+
+
+class Sweep:
+    """The rank-local part of a sweep (device closed loops + run summaries)."""
+
+    def __init__(self, scenario="radial", n_seeds=1, n_ics=1024, Nx=20, noise=(0.3, 0.3, 50),
+                 isReject=True, T_final=150.0, rank=0, world=1, device="cuda", shards=2,
+                 ic_seed=20250328, noise_seed=123, eps=1e-3, keep_traj=False):
+        import torch
+
+        from .closed_loop import ShardedClosedLoop
+
+        self.G = n_seeds * n_ics
+        self.lo, self.hi = launch.shard_range(self.G, rank, world)
+        self.sim, self.prob = build(scenario, Nx, noise, isReject, T_final)
+        self.nsim = int(self.sim.T_final / self.sim.time_stp)
+        X = scenario_states(scenario, n_seeds, n_ics, self.lo, self.hi, ic_seed)
+        # the reference's default OSQP tolerances (eps_abs = eps_rel = 1e-3) unless asked otherwise
+        self.loop = ShardedClosedLoop(self.prob, X, shards=shards, device=device, id_offset=self.lo,
+                                      noise=noise, noise_seed=noise_seed, eps_abs=eps, eps_rel=eps)
+        self.loop.enable_tracking(self.nsim, *self.sim.suc_cond)
+        self.traj = None
+        if keep_traj:
+            self.traj = torch.empty(self.hi - self.lo, self.nsim + 1, 4, dtype=torch.float64,
+                                    device=device)
+            self.traj[:, 0] = self.loop.x_true
+        self.steps = 0
+
+    def run(self, check_every=16):
+        """step every chaser until all terminated or the horizon (T_final / T) is reached"""
+        for k in range(self.nsim):
+            self.loop.step()
+            self.steps += 1
+            if self.traj is not None:
+                self.traj[:, k + 1] = self.loop.x_true
+            if (k + 1) % check_every == 0 and bool(self.loop.done.all()):
+                break
+        self.loop.synchronize()
+        return self
+
+    def summary(self):
+        return self.loop.summary()
+
+    def close(self):
+        self.loop.close()
+
+
+def reduce(S: np.ndarray):
+    """headline statistics of a gathered [G, 8] summary"""
+    f = {k: S[:, i] for i, k in enumerate(FIELDS)}
+    it = f["i_term"].astype(int)
+    hist, edges = np.histogram(it, bins=np.arange(0, it.max() + 21, 20))
+    st, cnt = np.unique(f["last_status"].astype(int), return_counts=True)
+    return dict(scenarios=int(S.shape[0]), success=int(f["success"].sum()),
+                success_rate=float(f["success"].mean()),
+                i_term_hist={int(e): int(h) for e, h in zip(edges[:-1], hist) if h},
+                i_term_mean=float(it.mean()), final_err_mean=float(f["final_err"].mean()),
+                final_err_median=float(np.median(f["final_err"])),
+                fallback_step_frac=float(f["n_fallback"].sum() / max(1, it.sum())),
+                admm_iters_total=float(f["admm_iters"].sum()),
+                last_status={int(a): int(b) for a, b in zip(st, cnt)})
+
+
+def main(argv=None):
+    argv = sys.argv if argv is None else argv
+    ap = argparse.ArgumentParser(prog="python -m mpc_arpo_project_amd.sweep")
+    ap.add_argument("--scenario", choices=("radial", "in_track"), default="radial")
+    ap.add_argument("--seeds", type=int, default=1024)
+    ap.add_argument("--ics", type=int, default=1024)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--nx", type=int, default=20)
+    ap.add_argument("--noise", default="0.3,0.3,50", help="sig_x,sig_y,noise_length or 'none'")
+    ap.add_argument("--no-reject", action="store_true")
+    ap.add_argument("--tfinal", type=float, default=150.0)
+    ap.add_argument("--eps", type=float, default=1e-3)
+    ap.add_argument("--shards", type=int, default=2)
+    ap.add_argument("--traj", action="store_true", help="gather trajectories to rank 0")
+    ap.add_argument("--out", default="", help="rank 0 saves the [G, 8] summary (.npy)")
+    a = ap.parse_args(argv[1:])
+    if a.gpus > 1 and not launch.launched():
+        return launch.relaunch(a.gpus, argv, module="mpc_arpo_project_amd.sweep")
+    import torch
+
+    rank, world, local, device, dist = launch.init("nccl")
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but {world} ranks were launched")
+    noise = None if a.noise == "none" else tuple(float(v) for v in a.noise.split(","))
+    if noise is not None:
+        noise = (noise[0], noise[1], int(noise[2]))
+    sw = Sweep(a.scenario, a.seeds, a.ics, Nx=a.nx, noise=noise, isReject=not a.no_reject,
+               T_final=a.tfinal, rank=rank, world=world, device=device, shards=a.shards,
+               eps=a.eps, keep_traj=a.traj)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sw.run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    local_sum = sw.summary()
+    S = launch.gather_rows(local_sum, sw.G, rank, world, dist)
+    traj = None
+    if a.traj:
+        traj = sw.traj
+        if dist:  # to rank 0 only (a gather, not an all-gather, for 1.2 GB per rank)
+            per = -(-sw.G // world)
+            pad = torch.zeros(per, sw.nsim + 1, 4, dtype=torch.float64, device=device)
+            pad[:traj.shape[0]] = traj
+            bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+            dist.gather(pad, bufs, dst=0)
+            if rank == 0:
+                traj = torch.cat([bufs[r][:launch.shard_range(sw.G, r, world)[1] -
+                                          launch.shard_range(sw.G, r, world)[0]]
+                                  for r in range(world)])
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        Sn = S.cpu().numpy()
+        out = reduce(Sn)
+        solved_steps = float(Sn[:, FIELDS.index("i_term")].sum())
+        out.update(scenario=a.scenario, n_gpus=world, seeds=a.seeds, ics=a.ics, nx=a.nx,
+                   noise=a.noise, reject=not a.no_reject, steps=sw.steps, seconds=el,
+                   scenarios_per_s=sw.G / el, solves_per_s=solved_steps / el)
+        if a.out:
+            np.save(a.out, Sn)
+            if traj is not None:
+                np.save(a.out.replace(".npy", "") + "_traj.npy", traj.cpu().numpy())
+        print(json.dumps(out), flush=True)
+    sw.close()
+    if dist:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -91,6 +91,10 @@ def lib():
         L.oqp_batch_update_solve.argtypes = [C.c_int, C.POINTER(C.c_void_p), dp, dp, dp, C.c_int,
                                              dp, ip, ip]
         L.oqp_batch_update_solve.restype = C.c_int
+        L.oqp_set_state.argtypes = [vp, dp, dp, dp, C.c_double]
+        L.oqp_set_state.restype = C.c_int
+        L.oqp_batch_set_state.argtypes = [C.c_int, C.POINTER(C.c_void_p), dp, dp, dp, dp]
+        L.oqp_batch_set_state.restype = C.c_int
         _lib = L
     return _lib
 
@@ -220,6 +224,13 @@ class OracleOSQP:
         return dict(x=xs, z=zs, y=ys, D=D, E=E, c=c.value, rho=lib().oqp_rho(self._w),
                     nnzL=lib().oqp_nnz_L(self._w))
 
+    def set_state(self, x, z, y, rho=0.0):
+        """overwrite the scaled iterates and rho (white-box hook: start from another solver's
+        state, e.g. the GPU engine's BatchQP.get_state())"""
+        x, z, y = (np.ascontiguousarray(a, dtype=np.float64) for a in (x, z, y))
+        if lib().oqp_set_state(self._w, _dp(x), _dp(z), _dp(y), float(rho)):
+            raise ValueError("refactorization failed")
+
     def __del__(self):
         if getattr(self, "_w", None) and _lib is not None:
             _lib.oqp_cleanup(self._w)
@@ -273,3 +284,12 @@ def batch_update_solve(solvers, Ax_batch, l_batch, u_batch, nthreads=1):
     it = np.empty(B, dtype=np.int32)
     lib().oqp_batch_update_solve(B, arr, pAx, pl, pu, nthreads, _dp(x), _ip(st), _ip(it))
     return x, st, it
+
+
+def batch_set_state(solvers, xs, zs, ys, rho):
+    """OracleOSQP.set_state for a list of solvers from [B, n] / [B, m] / [B] arrays."""
+    B = len(solvers)
+    arr = (C.c_void_p * B)(*[s._w for s in solvers])
+    xs, zs, ys, rho = (np.ascontiguousarray(a, dtype=np.float64) for a in (xs, zs, ys, rho))
+    if lib().oqp_batch_set_state(B, arr, _dp(xs), _dp(zs), _dp(ys), _dp(rho)):
+        raise ValueError("refactorization failed")

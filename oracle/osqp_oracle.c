@@ -1213,6 +1213,30 @@ void oqp_get_state(const oqp_work *w, double *x_s, double *z_s, double *y_s, dou
   if (c) *c = w->c;
 }
 
+/* White-box hook (parity characterisation only): overwrite the scaled warm-start iterates and
+ * rho with another solver's (e.g. the GPU engine's mpcqp_get_state), so that the next
+ * update + solve of both starts from bitwise-identical state.  A changed rho re-factors exactly as
+ * osqp_update_rho does. */
+int oqp_set_state(oqp_work *w, const double *x_s, const double *z_s, const double *y_s, double rho) {
+  if (x_s) memcpy(w->x, x_s, sizeof(double) * (size_t)w->n);
+  if (z_s) memcpy(w->z, z_s, sizeof(double) * (size_t)w->m);
+  if (y_s) memcpy(w->y, y_s, sizeof(double) * (size_t)w->m);
+  if (rho > 0 && rho != w->set.rho) return oqp_update_rho(w, rho);
+  return 0;
+}
+
+int oqp_batch_set_state(int B, oqp_work **works, const double *x_s, const double *z_s,
+                        const double *y_s, const double *rho) {
+  int rc = 0;
+  for (int b = 0; b < B; b++) {
+    oqp_work *w = works[b];
+    if (oqp_set_state(w, x_s + (size_t)b * w->n, z_s + (size_t)b * w->m, y_s + (size_t)b * w->m,
+                      rho[b]))
+      rc = 1;
+  }
+  return rc;
+}
+
 /* ---------------------------------------------------------------- batch driver */
 typedef struct {
   int b0, b1, n, m;

@@ -83,6 +83,13 @@ int oqp_nnz_L(const oqp_work *w);
 void oqp_get_state(const oqp_work *w, double *x_s, double *z_s, double *y_s, double *D, double *E,
                    double *c);
 
+/* overwrite the scaled iterates (x_s [n], z_s, y_s [m]; any may be NULL) and rho (<= 0: keep),
+ * re-factoring on a rho change (osqp_update_rho); the batch form takes [B*n] / [B*m] / [B] arrays.
+ * White-box parity characterisation only (start oracle and GPU from identical state). */
+int oqp_set_state(oqp_work *w, const double *x_s, const double *z_s, const double *y_s, double rho);
+int oqp_batch_set_state(int B, oqp_work **works, const double *x_s, const double *z_s,
+                        const double *y_s, const double *rho);
+
 /* Batch driver used as the CPU baseline and by the parity tests: for each instance b, set up a
  * solver on (P, q, A with values Ax[b], l[b], u[b]), solve it (cold), and store x/y/status/iter.
  * Instances are spread over `nthreads` POSIX threads.  Returns 0 on success. */

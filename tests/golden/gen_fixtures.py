@@ -12,7 +12,6 @@ How the vectors are made:
     the reference's own QP-construction code; the solutions are the oracle's;
   * batches of estimates from `scenarios.sample_estimates` are pushed through the reference's
     `configureDynamicConstraints` (pins the restated / device-side per-step reconfiguration);
-  * high-accuracy polished solutions of selected instances are KKT-certified here with numpy.
 Only the resulting arrays are committed; no reference source travels.
 """
 import os
@@ -106,23 +105,6 @@ def ref_objects(mod, Nx, isDeltaV, isReject=True, x0=(100., 10., 0., 0.)):
     return sim, mpc, fail, deb
 
 
-def certify(P, q, A, l, u, x, y, tol=1e-6):
-    """KKT certificate of a polished solution: primal feasibility, stationarity, sign-consistent
-    complementarity (y>0 only at upper-active rows, y<0 only at lower-active rows)."""
-    Ax = A @ x
-    scale = max(1.0, np.max(np.abs(Ax)))
-    lo = np.where(np.isfinite(l), l, -1e30)
-    hi = np.where(np.isfinite(u), u, 1e30)
-    prim = max(np.max(lo - Ax), np.max(Ax - hi), 0.0) / scale
-    g = P @ x + q + A.T @ y
-    gs = max(np.max(np.abs(P @ x)), np.max(np.abs(q)), np.max(np.abs(A.T @ y)), 1.0)
-    stat = np.max(np.abs(g)) / gs
-    ys = max(np.max(np.abs(y)), 1.0)
-    comp_up = np.max(np.where(y > tol * ys, np.abs(hi - Ax), 0.0)) / scale
-    comp_lo = np.max(np.where(y < -tol * ys, np.abs(Ax - lo), 0.0)) / scale
-    return dict(prim=prim, stat=stat, comp=max(comp_up, comp_lo))
-
-
 def main():
     install_stubs()
     import src.mpcsim as RM  # the reference's parameter classes
@@ -199,28 +181,7 @@ def main():
                             l=np.array(ls), u=np.array(us), A_indices=Ac0.indices,
                             A_indptr=Ac0.indptr)
         print(tag, "Ax", np.array(Axs).shape)
-
-        # ---------------- 3. certified solutions of the first 8 batch instances
-        su = out["cl_n20" if Nx == 20 else "cl_n40dv"][4]
-        P = su["P"]
-        Pt = orc.prepare_P(P)
-        xs, ys, objs, certs = [], [], [], []
-        for b in range(8):
-            A = sp.csc_matrix((Axs[b], Ac0.indices, Ac0.indptr), shape=Ac0.shape)
-            s = orc.OracleOSQP()
-            s.setup(P, su["q"], A, ls[b], us[b], eps_abs=1e-9, eps_rel=1e-9, max_iter=200000,
-                    polish=True, polish_refine_iter=10, warm_start=True, verbose=False)
-            r = s.solve()
-            c = certify(P, su["q"], A, ls[b], us[b], r.x, r.y)
-            xs.append(r.x)
-            ys.append(r.y)
-            objs.append(r.info.obj_val)
-            certs.append([c["prim"], c["stat"], c["comp"]])
-            print(tag, b, r.info.status, r.info.iter, "polish", r.info.status_polish, c,
-                  "u0", r.x[(Nx + 1) * 4:(Nx + 1) * 4 + 2])
-        np.savez_compressed(os.path.join(HERE, f"cert_{tag}.npz"), x=np.array(xs), y=np.array(ys),
-                            obj=np.array(objs), cert=np.array(certs), Pt_data=Pt.data)
-
+        # (certified optima: tests/golden/gen_certs.py, >= 248 instances per config)
 
 if __name__ == "__main__":
     main()

@@ -1,4 +1,4 @@
-"""Generates tests/golden/cl_noise_n20.npz, clc_n20.npz, clc_n40dv.npz.  CONTAINER-ONLY: needs
+"""Generates tests/golden/cl_noise_n20.npz, clc_n20.npz, clc_n40dv.npz, cl_intrack_n40.npz.  CONTAINER-ONLY: needs
 /root/reference (never on the GPU box).
 
 The reference's OWN closed-loop functions run unmodified; the third-party modules it imports
@@ -13,6 +13,8 @@ but which are absent from this image are replaced (as in gen_fixtures.py):
     global generator itself (src/trajectorySimulate.py:28).
   * clc_n20 / clc_n40dv: src.trajectorySimulateC.trajectorySimulateC, noise=None, T_cont = 1e-3
     (test/traj_eval_radialC.py:38), a 12 s horizon (12,000 solve_ivp sub-steps).
+  * cl_intrack_n40 (`python gen_fixtures_loops.py in_track`): trajectorySimulate on the in-track
+    approach of test/traj_eval_in_track.py (Nx = 40, swap_xy, noise=None).
 Only the resulting arrays are committed; no reference source travels.
 """
 import os
@@ -73,7 +75,47 @@ def run_record(fn, sim, mpc, fail, deb):
     return run, d
 
 
+def ref_objects_in_track(M, Nx=40):
+    """the reference's parameter classes with test/traj_eval_in_track.py's constants (Nx = 40,
+    swap_xy = True).  The script omits MPCParams' required u_lim (it would raise a TypeError as
+    written); (0.2, 0.2), the radial scripts' value, is supplied."""
+    import scipy.sparse as sp
+
+    sim = M.SimConditions(np.array([-10., 100., 0., 0.]), np.array([0., 2.5, 0., 0.]), 2.5,
+                          10 * (np.pi / 180), 1.5, 1.107e-3, 0.5, False, (0.2, 45), None, True)
+    Q = 8e+02 * sp.diags([0.2 ** 2., 10 ** 2., 3.8 ** 2, 900])
+    R = 1000 ** 2 * sp.diags([1, 1])
+    Rs = 5 ** 2 * sp.diags([1.5, 1.5, 1, 1, 1e5])
+    v = 50000 * np.ones(5)
+    v[-2] = -v[-2]
+    v[-1] = 1e-09
+    mpc = M.MPCParams(Q, R, Rs, v, {"Nx": Nx, "Nc": 5, "Nb": 5}, (0.2, 0.2), swap_xy=True)
+    fail = M.FailsafeParams(0.005 * np.diag([0.0001, 1, 100000., 1., 0.01]), 100 * np.diag([1, 1]),
+                            np.eye(1, 4), np.zeros([2, 2]))
+    deb = M.Debris((0., 40.), 5., 20)
+    return sim, mpc, fail, deb
+
+
+def in_track():
+    """cl_intrack_n40: the reference's trajectorySimulate on the in-track approach (noise=None),
+    covering the in-track quirk Q4 (src/simhelpers.py:69-75: x/y swapped in the estimate)."""
+    install_stubs()
+    import src.mpcsim as RM
+    from src.trajectorySimulate import trajectorySimulate
+
+    sim, mpc, fail, deb = ref_objects_in_track(RM)
+    run, d = run_record(trajectorySimulate, sim, mpc, fail, deb)
+    it = int(run.i_term)
+    d.update(x_est=run.x_est[:, :it + 1], ctrl_hist=run.ctrl_hist[:, :it + 1])
+    np.savez_compressed(os.path.join(HERE, "cl_intrack_n40.npz"), **d)
+    print("cl_intrack_n40 i_term", it, "success", run.isSuccess, "solves", len(d["solve_x"]),
+          "statuses", np.unique(d["solve_status"], return_counts=True),
+          "ctrl", np.unique(run.ctrlr_seq, return_counts=True))
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "in_track":
+        return in_track()
     install_stubs()
     import src.mpcsim as RM
     from src.trajectorySimulate import trajectorySimulate

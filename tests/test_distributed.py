@@ -59,3 +59,46 @@ def test_shard_ranges_cover_batch():
     parts = [bench.initial_states(world * B, r, B, 7) for r in range(world)]
     full = bench.initial_states(world * B, 0, world * B, 7)
     assert np.array_equal(np.vstack(parts), full)
+
+
+def _summary_rows(G, lo, hi):
+    """a deterministic per-scenario summary of global ids [lo, hi): the sweep's initial
+    conditions and the restated configure data's row sums (what a rank computes for its shard)"""
+    from mpc_arpo_project_amd import sweep
+
+    X = sweep.scenario_states("in_track", 4, G // 4, lo, hi, ic_seed=99)
+    g = np.arange(lo, hi, dtype=np.float64)[:, None]
+    return torch.as_tensor(np.hstack([g, X, X.sum(axis=1, keepdims=True) * g]))
+
+
+def _gather_worker(rank, world, port, G, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mpc_arpo_project_amd import launch
+
+    lo, hi = launch.shard_range(G, rank, world)
+    full = launch.gather_rows(_summary_rows(G, lo, hi), G, rank, world, dist)
+    if rank == 0:
+        torch.save(full, out_path)
+    dist.destroy_process_group()
+
+
+def test_summary_gather_matches_single_process(tmp_path):
+    """uneven shards (G = 4 x 13 over 3 ranks) gathered with launch.gather_rows equal the
+    single-process rows: the sweep's / bench's per-scenario summary path"""
+    world, G = 3, 52
+    out = str(tmp_path / "summ.pt")
+    mp.spawn(_gather_worker, args=(world, _free_port(), G, out), nprocs=world, join=True)
+    full = torch.load(out, weights_only=True)
+    assert torch.equal(full, _summary_rows(G, 0, G))
+
+
+def test_sweep_grid_and_in_track_ics():
+    from mpc_arpo_project_amd import sweep
+
+    ics = sweep.initial_conditions("in_track", 64, seed=3)
+    rad = sweep.initial_conditions("radial", 64, seed=3)
+    assert np.array_equal(ics[:, [1, 0, 2, 3]], rad)  # the radial geometry turned on its side
+    assert np.all(ics[:, 2:] == 0.0)
+    X = sweep.scenario_states("radial", 3, 64, 100, 140, ic_seed=3)
+    assert np.array_equal(X, rad[np.arange(100, 140) % 64])

@@ -72,3 +72,106 @@ def test_sharded_closed_loop_matches_single_stream(prob20):
     assert torch.equal(one.ctrl_seq, two.ctrl_seq)
     one.close()
     two.close()
+
+
+def test_sharded_read_after_step_without_sync(prob20):
+    """x_true / done / ctrl_seq read straight after step() (no explicit synchronize) are ordered
+    after the shards' side-stream writes"""
+    from mpc_arpo_project_amd.closed_loop import ShardedClosedLoop
+
+    X = scenarios.sample_estimates(64, seed=12)[:, :4]
+    X[:, 2:] = 0.0
+    one = BatchClosedLoop(prob20, X, eps_abs=1e-4, eps_rel=1e-4)
+    two = ShardedClosedLoop(prob20, X, shards=2, eps_abs=1e-4, eps_rel=1e-4)
+    for _ in range(4):
+        one.step()
+        two.step()
+        assert torch.equal(one.x_true.cpu(), two.x_true.cpu())
+        assert torch.equal(one.ctrl_seq.cpu(), two.ctrl_seq.cpu())
+    one.close()
+    two.close()
+
+
+def test_sharded_noisy_host_source_matches_single(prob20):
+    """a full-batch host noise source (numpy seeded generator, the reference's own draw) gives the
+    sharded loop the same draws as the unsharded one: the generator advances once per draw"""
+    from mpc_arpo_project_amd.closed_loop import ShardedClosedLoop
+
+    X = scenarios.sample_estimates(24, seed=13)[:, :4]
+    X[:, 2:] = 0.0
+    B = X.shape[0]
+
+    def source(seed):
+        rng = np.random.RandomState(seed)
+        calls = []
+
+        def draw(k):
+            calls.append(k)
+            return rng.normal(0, 1, (B, 4))
+        return draw, calls
+
+    d1, c1 = source(123)
+    d2, c2 = source(123)
+    one = BatchClosedLoop(prob20, X, noise=(0.05, 0.05, 2), noise_source=d1, eps_abs=1e-4,
+                          eps_rel=1e-4)
+    two = ShardedClosedLoop(prob20, X, shards=3, noise=(0.05, 0.05, 2), noise_source=d2,
+                            eps_abs=1e-4, eps_rel=1e-4)
+    for _ in range(6):
+        one.step()
+        two.step()
+    assert torch.equal(one.x_true.cpu(), two.x_true.cpu())
+    assert c1 == c2  # one host draw per noise index, whatever the shard count
+    one.close()
+    two.close()
+
+
+def test_in_track_device_loop_matches_reference_run(golden):
+    """the in-track approach (reference test/traj_eval_in_track.py: Nx = 40, swap_xy, quirk Q4 in
+    the device configure kernel) reproduces the reference's own run: controller sequence,
+    termination index, success flag and states; the tracked run summary agrees"""
+    from mpc_arpo_project_amd import qp_model
+
+    d = golden("cl_intrack_n40")
+    sim, mpc, fail, deb = scenarios.in_track_scenario(Nx=40, T_final=100)
+    prob = qp_model.build_problem(sim, mpc, fail, deb)
+    cl = BatchClosedLoop(prob, np.array([[-10., 100., 0., 0.]]))
+    nsim = int(sim.T_final / sim.time_stp)
+    cl.enable_tracking(nsim, *sim.suc_cond)
+    iterm = int(d["i_term"])
+    xs = [cl.x_true.cpu().numpy()[0].copy()]
+    for i in range(iterm):
+        r = cl.step()
+        assert int(r.status[0]) == int(d["solve_status"][i]) or \
+            (int(r.status[0]) != 1 and int(d["solve_status"][i]) != 1), i
+        assert int(cl.ctrl_seq[0]) == int(d["ctrlr_seq"][i]), i
+        xs.append(cl.x_true.cpu().numpy()[0].copy())
+    xs = np.array(xs).T
+    assert np.max(np.abs(xs[:, :iterm] - d["x_true_pcw"])) < 1e-6
+    assert int(cl.done[0]) == 1
+    s = cl.summary().cpu().numpy()[0]
+    f = dict(zip(cl.SUMMARY_FIELDS, s))
+    assert int(f["i_term"]) == iterm
+    assert bool(f["success"]) == bool(d["isSuccess"])
+    assert int(f["n_fallback"]) == int(np.sum(d["ctrlr_seq"] != 1))
+    xr = np.asarray(sim.xr, dtype=float)
+    assert abs(f["final_err"] - np.linalg.norm(d["x_true_pcw"][:, iterm - 1] - xr)) < 1e-9
+    cl.close()
+    run = trajectorySimulate(sim, mpc, fail, deb)  # the host mirror on the HIP engine
+    assert run.i_term == iterm and run.isSuccess == bool(d["isSuccess"])
+    assert np.array_equal(run.ctrlr_seq, d["ctrlr_seq"])
+
+
+def test_tracked_summary_matches_reference_radial_run(golden, prob20):
+    """run summary of the radial reference run (i_term 182, success) from the device tracking"""
+    d = golden("cl_n20")
+    cl = BatchClosedLoop(prob20, np.array([[100., 10., 0., 0.]]))
+    cl.enable_tracking(300, 0.2, 45.0)
+    iterm = int(d["i_term"])
+    for _ in range(iterm + 3):  # steps past termination leave the summary unchanged
+        cl.step()
+    f = dict(zip(cl.SUMMARY_FIELDS, cl.summary().cpu().numpy()[0]))
+    assert int(f["i_term"]) == iterm
+    assert bool(f["success"]) == bool(d["isSuccess"])
+    assert int(f["admm_iters"]) == int(np.sum(d["solve_iter"][:iterm]))
+    assert abs(f["final_err"] - np.linalg.norm(d["x_true_pcw"][:, iterm - 1] - [2.5, 0, 0, 0])) < 1e-9
+    cl.close()

@@ -2,8 +2,8 @@
 
 Tolerances (fp64 path, north star: ||u* - u*_ref||_inf < 1e-5 at eps_abs = 1e-6):
   * status and ADMM iteration counts: identical to the oracle;
-  * u0 = x[(Nx+1)nx : (Nx+1)nx+nu]: < 1e-8 vs the oracle at the same settings, < 1e-5 vs the
-    KKT-certified solution at eps = 1e-6;
+  * u0 = x[(Nx+1)nx : (Nx+1)nx+nu]: < 1e-8 vs the oracle at the same settings (the north-star
+    eps = 1e-6 comparison and the certified optima: tests/test_gpu_scale_parity.py);
   * full x: relative error < 1e-6.
 """
 import numpy as np
@@ -51,19 +51,6 @@ def test_batch_fixture_parity_eps1e4(golden, Nx, dv, tag):
     _compare(prob, r, ref)
     # the fixture set covers solved, solved-inaccurate, max-iter and primal-infeasible instances
     assert {1, -3}.issubset(set(ref[2].tolist()))
-
-
-def test_north_star_tolerance_eps1e6(golden, prob20):
-    d = golden("batch_n20")
-    c = golden("cert_batch_n20")
-    st = dict(eps_abs=1e-6, eps_rel=1e-6, max_iter=20000)
-    r, ref = _solve_both(prob20, d["Ax"][:8], d["l"][:8], d["u"][:8], **st)
-    _compare(prob20, r, ref, u0_tol=1e-5)
-    xg = r.x.cpu().numpy()
-    sl = prob20.u0_slice
-    for b in range(8):
-        if np.all(np.isfinite(c["x"][b])) and np.max(c["cert"][b]) < 1e-8 and ref[2][b] == 1:
-            assert np.max(np.abs(xg[b, sl] - c["x"][b][sl])) < 1e-5
 
 
 def test_closed_loop_update_sequence_replay(golden, prob20):
@@ -142,31 +129,6 @@ def test_osqp_compat_errors(prob20):
     res = s.solve()
     assert res.info.status == "solved"
     assert torch.cuda.is_available()
-
-
-def test_dense_engine_opt_in(golden, monkeypatch):
-    """MPCQP_ENGINE=dense: the dense-inverse engine (explicit M^-1, dense.hip) takes the same ADMM
-    steps up to the inverse's rounding: statuses of the fixture set equal the oracle's, iteration
-    counts agree on nearly all instances, u0 within 1e-6 on instances both solve"""
-    from conftest import problem
-
-    prob = problem(20, False)
-    d = golden("batch_n20")
-    monkeypatch.setenv("MPCQP_ENGINE", "dense")
-    st = dict(eps_abs=1e-4, eps_rel=1e-4)
-    qp = BatchQP(prob.P, prob.A, batch=d["Ax"].shape[0], **st)
-    assert qp.schedule_info()["engine"] == "dense"
-    qp.set_data(q=prob.q, Ax=d["Ax"], l=d["l"], u=d["u"])
-    r = qp.solve()
-    xo, yo, so, io = orc.batch_solve(prob.P, prob.q, prob.A, d["Ax"], d["l"], d["u"], nthreads=8, **st)
-    sg, ig, xg = r.status.cpu().numpy(), r.iter.cpu().numpy(), r.x.cpu().numpy()
-    assert np.array_equal(sg, so), (sg, so)
-    assert np.mean(ig == io) >= 0.9, (ig, io)
-    ok = (so == 1) & (sg == 1)
-    sl = prob.u0_slice
-    assert np.max(np.abs(xg[ok][:, sl] - xo[ok][:, sl])) < 1e-6
-    monkeypatch.delenv("MPCQP_ENGINE")
-    assert BatchQP(prob.P, prob.A, batch=4, **st).schedule_info()["engine"] == "kkt"
 
 
 def test_repeated_solves_are_bit_identical(golden):

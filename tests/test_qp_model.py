@@ -81,3 +81,32 @@ def test_in_track_problem_builds():
         a1, li, ui = qp_model.configure_dynamic_constraints(prob, X[b].copy())
         assert np.array_equal(a1, Ax[b])
         assert np.array_equal(qp_model.full_bounds(prob, X[b], li, ui)[0], l[b])
+
+
+def _prob_in_track():
+    from conftest import _PROBS
+
+    if "intrack40" not in _PROBS:
+        sim, mpc, fail, deb = scenarios.in_track_scenario(Nx=40, T_final=100)
+        _PROBS["intrack40"] = qp_model.build_problem(sim, mpc, fail, deb)
+    return _PROBS["intrack40"]
+
+
+def test_in_track_setup_and_updates_bit_exact(golden):
+    """the in-track approach (reference test/traj_eval_in_track.py, Nx = 40, swap_xy): set-up data
+    and every per-step update the reference issued, reproduced bit for bit -- including quirk Q4
+    (src/simhelpers.py:69-75: configureDynamicConstraints swaps x / y of the caller's estimate in
+    place, so the reference's recorded estimates are the swapped ones)"""
+    d = golden("cl_intrack_n40")
+    prob = _prob_in_track()
+    assert np.array_equal(d["setup_l"], prob.l) and np.array_equal(d["setup_u"], prob.u)
+    assert np.array_equal(d["A_data"], prob.A.data)
+    xe = d["x_est"]
+    for i in range(d["step_Ax"].shape[0]):
+        x = xe[:, i + 1].copy()
+        x[[0, 1]] = x[[1, 0]]  # undo the in-place swap the reference's call left behind
+        Ax, li, ui = qp_model.configure_dynamic_constraints(prob, x, swap_in_place=True)
+        assert np.array_equal(x, xe[:, i + 1])  # ... which the restatement reproduces
+        l, u = qp_model.full_bounds(prob, xe[:, i + 1][[1, 0, 2, 3, 4, 5]], li, ui)
+        assert np.array_equal(Ax, d["step_Ax"][i]), i
+        assert np.array_equal(l, d["step_l"][i]) and np.array_equal(u, d["step_u"][i]), i

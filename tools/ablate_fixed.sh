@@ -13,7 +13,7 @@ if [ "$1" = build ]; then
     F="-DEXP_NOCHECK"; [ $v != base ] && F="$F -DEXP_$v"
     [ $v = CHECK_NOEXIT ] && F="-DEXP_CHECK_NOEXIT"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -DMPCQP_ONLY_SMALL $F \
-      $C/engine.hip $C/dense.hip $C/dense_plan.cpp $C/closed_loop.hip $C/estimation.hip $C/symbolic.cpp \
+      $C/engine.hip $C/closed_loop.hip $C/estimation.hip $C/symbolic.cpp \
       -o "$R/tools/abl/libmpcqp_$v.so" 2>&1 | grep -v hip-link &
   done
   wait; ls -la "$R/tools/abl"

@@ -17,11 +17,3 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$O/prof_bench.json" 2> "$O/prof_bench.err" || { echo prof failed; tail -20 "$O/prof_bench.err"; exit 1; }
 cat "$O/prof_bench.json"
 find "$O/prof" -name "*stats*"
-# diagnostics: phase timing of both engines, dense-engine bench
-if [ -f "$R/tools/libmpcqp_timing.so" ]; then
-  cd "$R"
-  timeout -k 10 300 python tools/phase_timing.py run 65536 5 > "$O/phase_kkt.json" 2> "$O/phase_kkt.err" || { echo phase failed; tail -5 "$O/phase_kkt.err"; exit 1; }
-  MPCQP_ENGINE=dense timeout -k 10 300 python tools/phase_timing.py run 65536 5 > "$O/phase_dense.json" 2> "$O/phase_dense.err" || { echo phase dense failed; tail -5 "$O/phase_dense.err"; exit 1; }
-  MPCQP_ENGINE=dense timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 > "$O/bench_dense.json" 2> "$O/bench_dense.err" || { echo dense bench failed; exit 1; }
-  cat "$O/bench_dense.json"
-fi

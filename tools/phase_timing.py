@@ -21,8 +21,8 @@ SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfac
 def build(extra=()):
     csrc = os.path.join(REPO, "mpc_arpo_project_amd", "csrc")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-DMPCQP_TIMING", *extra, os.path.join(csrc, "engine.hip"), os.path.join(csrc, "dense.hip"),
-           os.path.join(csrc, "dense_plan.cpp"), os.path.join(csrc, "closed_loop.hip"),
+           "-DMPCQP_TIMING", *extra, os.path.join(csrc, "engine.hip"),
+           os.path.join(csrc, "closed_loop.hip"),
            os.path.join(csrc, "estimation.hip"),
            os.path.join(csrc, "symbolic.cpp"), "-o", LIB]
     subprocess.check_call(cmd)
@@ -59,17 +59,6 @@ def run(B=65536, steps=5, warmup=3, nx=20):
         torch.cuda.synchronize()
         kt += ev0.elapsed_time(ev1)
     t = dict(zip(SLOTS, buf.cpu().tolist()))
-    if cl.qp.schedule_info()["engine"] == "dense":
-        ds = ["scale", "form", "sweep", "rhs", "matvec", "zupd", "check", "iters", "nfact"]
-        td = dict(zip(ds, buf.cpu().tolist()))
-        n_inst = B * steps
-        out = {"engine": "dense", "B": B, "kernel_ms_per_launch": None,
-               "iters_per_solve": td["iters"] / n_inst,
-               "cycles_per_solve": {k: td[k] / n_inst for k in ds[:7]},
-               "cycles_per_iter": {k: td[k] / max(td["iters"], 1) for k in ("rhs", "matvec", "zupd", "check")},
-               "cycles_per_factorization": {k: td[k] / max(td["nfact"], 1) for k in ("form", "sweep")}}
-        print(json.dumps(out, indent=1))
-        return
     n_inst = B * steps
     iters = t["iters"]
     sched = cl.qp.schedule_info()
