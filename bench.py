@@ -127,7 +127,7 @@ def cpu_baseline(prob, X0, steps, warmup, eps, sample, threads, device):
         fast_agree.append(float(np.mean(same[fast])) if fast.any() else 1.0)
     timed = max(steps if warmup >= 1 else steps - 1, 1)
     return dict(value=S * timed / t_cpu, unit="solves/s", cores=threads, kind="port",
-                cgroup_cpu_quota=cgroup_cpus(),
+                affinity_cpus=len(os.sched_getaffinity(0)), cgroup_cpu_quota=cgroup_cpus(),
                 sample=f"{S} chasers x {timed} warm closed-loop steps (update(l,u)+update(Ax)+solve, "
                        f"eps {eps:g}) after {warmup} untimed steps; {t_cpu:.2f} s on {threads} "
                        f"threads",
@@ -363,7 +363,12 @@ def main(argv=None):
     }
     if world == 1 and not args.no_cpu_baseline:
         try:
-            thr = args.cpu_threads or len(os.sched_getaffinity(0))
+            # every core this process may run on: the affinity mask, capped by the cgroup CPU
+            # quota when one is set (the GPU box grants 16 CPUs of a 256-thread host: 256 threads
+            # on a 16-CPU quota measured 2.3x slower than 16)
+            aff = len(os.sched_getaffinity(0))
+            quota = cgroup_cpus()
+            thr = args.cpu_threads or (min(aff, int(quota)) if quota and quota >= 1 else aff)
             out["cpu_baseline"] = cpu_baseline(prob, X0, K, args.warmup, args.eps, args.cpu_sample,
                                                thr, device)
         except Exception as e:  # report, never fake

@@ -2,9 +2,9 @@
 // include/mpcqp_closed_loop.h).  One thread per chaser; this is scalar per-instance logic, a few
 // hundred bytes of traffic per instance and step, far off the solve's critical path.
 //
-// Arithmetic that feeds comparisons with the reference (slopes, intercepts, norms, the plant) uses
-// explicitly rounded operations (__dmul_rn / __dadd_rn) in the reference's evaluation order, so
-// that no FMA contraction changes a branch the reference would take.
+// Arithmetic that feeds comparisons with the reference (slopes, intercepts, norms, the plant) is
+// evaluated in the reference's order with FP contraction off (see mul / add below), so the
+// controller, plant and QP reconfiguration reproduce the reference's floating-point results.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,9 +36,28 @@ struct ClDev {
   Track tr;
 };
 
-__device__ __forceinline__ double mul(double a, double b) { return __dmul_rn(a, b); }
-__device__ __forceinline__ double add(double a, double b) { return __dadd_rn(a, b); }
-__device__ __forceinline__ double sub(double a, double b) { return __dsub_rn(a, b); }
+// No FMA contraction in this file's own arithmetic (hipcc contracts a * b + c by default, and
+// __dmul_rn / __dadd_rn are plain operators in ROCm's headers, so they fuse too): the scalar logic
+// below restates numpy / scipy operation by operation, and a fused multiply-add rounds once where
+// the reference rounds twice.  Fused operations appear only where numpy's own kernels fuse
+// (norm2 / norm4, __fma_rn).
+#pragma clang fp contract(off)
+__device__ __forceinline__ double mul(double a, double b) { return a * b; }
+__device__ __forceinline__ double add(double a, double b) { return a + b; }
+__device__ __forceinline__ double sub(double a, double b) { return a - b; }
+
+// numpy's evaluation orders on the reference's host (numpy 2.2 + OpenBLAS, measured bit for bit in
+// tests/test_closed_loop_host.py): np.linalg.norm of a short vector is sqrt of the OpenBLAS ddot
+// FMA chain; a 2x4 @ 4 product (dgemv) sums the four products as (a0 + a2) + (a1 + a3)
+__device__ __forceinline__ double norm2(double x0, double x1) {
+  return sqrt(__fma_rn(x1, x1, mul(x0, x0)));
+}
+__device__ __forceinline__ double norm4(const double* v) {
+  return sqrt(__fma_rn(v[3], v[3], __fma_rn(v[2], v[2], __fma_rn(v[1], v[1], mul(v[0], v[0])))));
+}
+__device__ __forceinline__ double dot4(const double* k, const double* x) {
+  return add(add(mul(k[0], x[0]), mul(k[2], x[2])), add(mul(k[1], x[1]), mul(k[3], x[3])));
+}
 
 // configureDynamicConstraints (reference src/simhelpers.py:66-138) for one chaser
 __global__ void __launch_bounds__(256) cl_configure_kernel(ClDev d, double* xest, double* Ax,
@@ -115,26 +134,14 @@ __device__ __forceinline__ int select_control(const mpcqp_cl_scenario& s, int32_
                         sub(xe[0], sub(s.center[0], h)) > 0 && xe[1] < add(s.center[1], h) &&
                         xe[1] > sub(s.center[1], h);
     if (in_box) {  // deadbeat debris avoidance
-      double cy = 0.0;
-      for (int k = 0; k < NX; ++k) cy = add(cy, mul(s.Crefy[k], xe[k]));
-      xi = sub(add(xi, cy), add(s.center[1], h));
-      c0 = sub(-(add(add(add(mul(s.Ktot[0], xe[0]), mul(s.Ktot[1], xe[1])), mul(s.Ktot[2], xe[2])),
-                     mul(s.Ktot[3], xe[3]))),
-               mul(s.Ki[0], xi));
-      c1 = sub(-(add(add(add(mul(s.Ktot[4], xe[0]), mul(s.Ktot[5], xe[1])), mul(s.Ktot[6], xe[2])),
-                     mul(s.Ktot[7], xe[3]))),
-               mul(s.Ki[1], xi));
+      xi = sub(add(xi, dot4(s.Crefy, xe)), add(s.center[1], h));
+      c0 = sub(-dot4(s.Ktot, xe), mul(s.Ki[0], xi));
+      c1 = sub(-dot4(s.Ktot + 4, xe), mul(s.Ki[1], xi));
       seq = 3;
     } else {  // LQR failsafe (homing)
-      double cxr = 0.0;
-      for (int k = 0; k < NX; ++k) cxr = add(cxr, mul(s.Crefx[k], xe[k]));
-      xi = sub(add(xi, cxr), s.xr[0]);
-      c0 = sub(-(add(add(add(mul(s.Kpf[0], xe[0]), mul(s.Kpf[1], xe[1])), mul(s.Kpf[2], xe[2])),
-                     mul(s.Kpf[3], xe[3]))),
-               mul(s.Kif[0], xi));
-      c1 = sub(-(add(add(add(mul(s.Kpf[4], xe[0]), mul(s.Kpf[5], xe[1])), mul(s.Kpf[6], xe[2])),
-                     mul(s.Kpf[7], xe[3]))),
-               mul(s.Kif[1], xi));
+      xi = sub(add(xi, dot4(s.Crefx, xe)), s.xr[0]);
+      c0 = sub(-dot4(s.Kpf, xe), mul(s.Kif[0], xi));
+      c1 = sub(-dot4(s.Kpf + 4, xe), mul(s.Kif[1], xi));
       seq = 2;
     }
   } else {
@@ -145,10 +152,10 @@ __device__ __forceinline__ int select_control(const mpcqp_cl_scenario& s, int32_
   }
   // input-norm clip with the reference's sequential rescale (quirk Q2)
   const double um = s.umax[0];
-  double nr = sqrt(add(mul(c0, c0), mul(c1, c1)));
+  double nr = norm2(c0, c1);
   if (nr > um) {
     c0 = mul(c0, um / nr);
-    nr = sqrt(add(mul(c0, c0), mul(c1, c1)));
+    nr = norm2(c0, c1);
     c1 = mul(c1, um / nr);
   }
   return seq;
@@ -157,14 +164,14 @@ __device__ __forceinline__ int select_control(const mpcqp_cl_scenario& s, int32_
 // termination test at the top of a loop iteration (src/trajectorySimulate.py:288-293,
 // src/trajectorySimulateC.py:328-333)
 __device__ __forceinline__ bool terminated(const mpcqp_cl_scenario& s, const double* x) {
-  const double rn = sqrt(add(mul(x[0], x[0]), mul(x[1], x[1])));
+  const double rn = norm2(x[0], x[1]);
   const double pos = s.inTrack ? x[1] : x[0];
   return rn < s.rp || pos < sub(s.rp, s.rtol);
 }
 
 // range / bearing measurement hx (src/trajectorySimulate.py:330-332)
 __device__ __forceinline__ void measure(const double* x, double* z) {
-  z[0] = sqrt(add(mul(x[0], x[0]), mul(x[1], x[1])));
+  z[0] = norm2(x[0], x[1]);
   z[1] = atan2(x[1], x[0]);
 }
 
@@ -195,16 +202,12 @@ __global__ void __launch_bounds__(256) cl_step_kernel(ClDev d, const int32_t* st
     // the reference's run reduction (src/trajectorySimulate.py:369-376 success test over the
     // states 1 .. iterm-1 of the run; test/disturbRejComp.py:88 final error |x(iterm-1) - xr|)
     const double* x = x_true + (size_t)b * NX;
-    const double e0 = sub(x[0], s.xr[0]), e1 = sub(x[1], s.xr[1]);
-    const double dist = sqrt(add(mul(e0, e0), mul(e1, e1)));
+    const double dist = norm2(sub(x[0], s.xr[0]), sub(x[1], s.xr[1]));
     const double ang = mul(fabs(atan(x[3] / x[2])), tr.rad2deg);
     if (tr.step >= 1 && dist <= tr.dist_tol && ang <= tr.ang_tol) tr.success[b] = 1;
-    double e2 = 0.0;
-    for (int k = 0; k < NX; ++k) {
-      const double ek = sub(x[k], s.xr[k]);
-      e2 = add(e2, mul(ek, ek));
-    }
-    tr.final_err[b] = sqrt(e2);
+    double e[NX];
+    for (int k = 0; k < NX; ++k) e[k] = sub(x[k], s.xr[k]);
+    tr.final_err[b] = norm4(e);
     if (seq != 1) tr.n_fallback[b] += 1;
   }
   ctrl_out[(size_t)b * 2] = c0;
@@ -305,23 +308,6 @@ __global__ void __launch_bounds__(64) clc_period_kernel(
   const int seq = select_control(s, status[b], x_sol + (size_t)b * n + u0, xe, xi, c0, c1);
   xintf[b] = xi;
   ctrl_seq[b] = seq;
-  const Track& tr = d.tr;
-  if (tr.iterm) {
-    // the reference's run reduction (src/trajectorySimulate.py:369-376 success test over the
-    // states 1 .. iterm-1 of the run; test/disturbRejComp.py:88 final error |x(iterm-1) - xr|)
-    const double* x = x_true + (size_t)b * NX;
-    const double e0 = sub(x[0], s.xr[0]), e1 = sub(x[1], s.xr[1]);
-    const double dist = sqrt(add(mul(e0, e0), mul(e1, e1)));
-    const double ang = mul(fabs(atan(x[3] / x[2])), tr.rad2deg);
-    if (tr.step >= 1 && dist <= tr.dist_tol && ang <= tr.ang_tol) tr.success[b] = 1;
-    double e2 = 0.0;
-    for (int k = 0; k < NX; ++k) {
-      const double ek = sub(x[k], s.xr[k]);
-      e2 = add(e2, mul(ek, ek));
-    }
-    tr.final_err[b] = sqrt(e2);
-    if (seq != 1) tr.n_fallback[b] += 1;
-  }
   ctrl_out[(size_t)b * 2] = c0;
   ctrl_out[(size_t)b * 2 + 1] = c1;
   double* up = ctrl_prev + (size_t)b * NU;

@@ -165,7 +165,7 @@ class BatchQP:
         entry are skipped by every following solve (outputs and warm state unchanged)"""
         if mask is not None:
             if mask.dtype != torch.int32 or tuple(mask.shape) != (self.B,) or \
-                    mask.device != self.device or not mask.is_contiguous():
+                    not mask.is_cuda or not mask.is_contiguous():
                 raise ValueError(f"skip mask must be a contiguous int32 tensor of shape ({self.B},)")
         check(_lib.lib().mpcqp_set_skip(self._h, None if mask is None else mask.data_ptr()),
               "mpcqp_set_skip")

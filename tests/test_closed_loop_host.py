@@ -18,3 +18,32 @@ def test_trajectory_matches_reference_loop(golden):
     assert np.array_equal(run.ctrl_hist[:, :run.i_term + 1], d["ctrl_hist"])
     assert np.array_equal(run.ctrlr_seq, d["ctrlr_seq"])
     assert np.array_equal(run.x_est[:, :run.i_term + 1], d["x_est"])
+
+
+def _fma(a, b, c):
+    from fractions import Fraction
+
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def test_numpy_evaluation_orders_the_device_kernels_follow(prob20):
+    """the closed-loop kernels (csrc/closed_loop.hip norm2 / norm4 / dot4) restate how numpy on
+    this image evaluates the reference's np.linalg.norm and 2x4 @ 4 products: the OpenBLAS ddot
+    FMA chain and the dgemv sum (a0 + a2) + (a1 + a3) -- bit for bit on random inputs"""
+    import math
+
+    rng = np.random.default_rng(7)
+    Kf = rng.normal(0, 1, (2, 5))
+    Kpf = Kf[:, :4]  # a non-contiguous slice, as the reference's Kf[:, :nx]
+    for K in (Kpf, np.asarray(prob20.Kpf), np.asarray(prob20.K_total)):
+        for _ in range(200):
+            x = rng.normal(0, 30, 4)
+            ref = K @ x
+            for r in range(2):
+                a = K[r] * x
+                assert ref[r] == (a[0] + a[2]) + (a[1] + a[3])
+    for _ in range(500):
+        v = rng.normal(0, 0.3, 4)
+        assert np.linalg.norm(v[:2]) == math.sqrt(_fma(v[1], v[1], v[0] * v[0]))
+        s4 = _fma(v[3], v[3], _fma(v[2], v[2], _fma(v[1], v[1], v[0] * v[0])))
+        assert np.linalg.norm(v) == math.sqrt(s4)
