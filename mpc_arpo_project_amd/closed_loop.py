@@ -112,6 +112,7 @@ class BatchClosedLoop:
         self.xintf = torch.zeros(self.B, **f)
         self.done = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self.ctrl_seq = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self.aborted = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         rn = np.hypot(x0[:, 0], x0[:, 1])
         pos = x0[:, 1] if prob.inTrack else x0[:, 0]
         self.done[:] = torch.as_tensor(((rn < prob.rp) | (pos < prob.rp - prob.rtol)).astype(np.int32))
@@ -162,10 +163,17 @@ class BatchClosedLoop:
         return self.noise[0], self.noise[1]
 
     def _estimate(self):
-        """UKF step on the measurement the plant kernel produced, estimate -> xest"""
+        """UKF step on the measurement the plant kernel produced, estimate -> xest.  A chaser whose
+        UKF covariance stops being positive definite is frozen as aborted: filterpy raises
+        numpy.linalg.LinAlgError there and the reference's run ends with that exception."""
         self.ukf.step(self.u_applied, self.z, active=self.ctrl_seq)
         with torch.cuda.stream(self.qp.stream):
             self.xest.copy_(self.ukf.x)
+            bad = ((self.ukf.status != 0) & (self.done == 0)).to(torch.int32)
+            self.aborted.bitwise_or_(bad)
+            self.done.bitwise_or_(bad)
+            if getattr(self, "_tracking", False):
+                self.iterm.copy_(torch.where(bad > 0, self.steps + 1, self.iterm))
 
     def step(self):
         """Solve the current QPs, apply the controller and plant, rebuild the QP data (async)."""
@@ -195,17 +203,18 @@ class BatchClosedLoop:
         self._tracking = True
 
     SUMMARY_FIELDS = ("u0_x", "u0_y", "last_status", "admm_iters", "i_term", "success",
-                      "final_err", "n_fallback")
+                      "final_err", "n_fallback", "aborted")
 
     def summary(self):
-        """(B, 8) float64 device tensor, columns SUMMARY_FIELDS (ordered after this loop's stream)"""
+        """(B, 9) float64 device tensor, columns SUMMARY_FIELDS (ordered after this loop's stream)"""
         if not getattr(self, "_tracking", False):
             raise MPCQPError("enable_tracking() first")
         torch.cuda.current_stream(self.device).wait_stream(self.qp.stream)
         return torch.cat([self.u0_first, self.last_status[:, None].double(),
                           self.iters_total[:, None].double(), self.iterm[:, None].double(),
                           self.success[:, None].double(), self.final_err[:, None],
-                          self.n_fallback[:, None].double()], dim=1)
+                          self.n_fallback[:, None].double(), self.aborted[:, None].double()],
+                         dim=1)
 
     def _track_solve(self, r):
         with torch.cuda.stream(self.qp.stream):
