@@ -58,6 +58,7 @@ struct DevPlan {
   const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
   int n, m, nk, nnzP, nnzA, nnzL;
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
+  int DS;  // D scratch of the factorization (overlays the block-inverse region)
   int NKS;  // 64-lane slots of the padded 1/D, W and C regions (symbolic.hpp NKP / 64 = RN + RM)
   // scaling index overlay (symbolic.hpp): 16-byte chunks copied to LDS at u16 offset SCI
   const uint4* sci_src;
@@ -378,7 +379,7 @@ __device__ __forceinline__ void run_fac(const uint32_t* tbl, int nsteps, double*
 // numeric LDL': U = L D and D by levels, L = U / D (flat pass), then the block-inverse tail
 __device__ __forceinline__ void run_factor(const KParams& p, double* v, int lane) {
   const DevPlan& P = p.pl;
-  const uint32_t dshift = (uint32_t)(P.DINV - P.W) * 8u;
+  const uint32_t dshift = (uint32_t)(P.DINV - P.DS) * 8u;  // may wrap: DINV precedes DS
   run_fac(P.fac, P.nfac, v, lane, dshift);
   LDS_FENCE();
 #pragma unroll 4
@@ -611,7 +612,7 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
                                     const Inst<RN, RM>& S) {
   const DevPlan& P = p.pl;
   for (int k = lane; k < P.nnzL; k += 64) v[P.LX + k] = 0.0;
-  for (int k = lane; k < P.nk; k += 64) v[P.W + k] = 0.0;
+  for (int k = lane; k < P.nk; k += 64) v[P.DS + k] = 0.0;
   if (lane == 0) {
     v[P.ZERO] = 0.0;
     v[P.ONE] = 1.0;
@@ -1315,8 +1316,13 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 }
 
 // One wave per workgroup; the instance image is the workgroup's whole (dynamic) LDS, at address 0.
+// MPCQP_WAVES_PER_EU: minimum waves per SIMD the register allocation must allow (1: up to 512
+// VGPRs + AGPRs per lane; 2: at most 256)
+#ifndef MPCQP_WAVES_PER_EU
+#define MPCQP_WAVES_PER_EU 1
+#endif
 template <int RN, int RM>
-__global__ void __launch_bounds__(64) qp_batch_kernel(KParams p) {
+__global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = (int)threadIdx.x;
   if ((uint32_t)(uintptr_t)lds != 0u) __builtin_trap();  // schedule byte addresses assume base 0
@@ -1534,6 +1540,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.nnzL = pl.nnzL;
     dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.CACC = pl.CACC, dp.ZERO = pl.ZERO;
     dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N, dp.NKS = pl.NKP / 64;
+    dp.DS = pl.DS;
     dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
     dp.sci_src = (const uint4*)(b + o_sci), dp.SCI = pl.SCI, dp.S_ZERO = pl.S_ZERO;
     dp.sci_n16 = (int)(pl.sci_block.size() / 8);

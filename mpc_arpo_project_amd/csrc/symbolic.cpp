@@ -226,17 +226,26 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
   return nsteps;
 }
 
-// Permute the LDS slots of the matrix values (L and the N | G | G' region) so that the matrix
-// operand reads of the solve steps are free of bank conflicts as far as possible: every value is
-// given a bank class (slot mod 32) that the other values read by the same instruction half do not
-// use (values read by both solves get the class that collides least), then the classes are mapped
-// to the region's slots.  All schedule records and assembly maps are rewritten.
-void layout_matrix_values(Plan& pl) {
-  const int nL = pl.nnzL, nM = pl.ZERO - pl.NB;
+// Map the construction-time layout (disjoint regions: L | 1/D | W | C | N G G' | consts | sinks |
+// D scratch) onto the final, overlaid LDS image (symbolic.hpp Plan) and rewrite every schedule
+// record and assembly map:
+//   * L: the entries the solves read (far-block couplings) take the first nLlive slots, the rest
+//     follow; W and C are placed over the solve-dead entries (the solves never read them, the
+//     factorization rewrites them all);
+//   * N | G | G' keep their region; the D scratch overlays its start (D is dead once the tail that
+//     writes N, G, G' starts);
+//   * the 64 sink slots go to the padding of W and C (written only with zeros by unused segments);
+//   * inside the L-live and N | G | G' ranges the values are permuted so that the matrix operand
+//     reads of the solve steps avoid LDS bank conflicts: every value gets a bank class (slot
+//     mod 32) that the other values read by the same instruction half do not use (values read by
+//     both solves get the class that collides least).
+void relocate(Plan& pl, bool conflict_layout) {
+  const int nL = pl.nnzL, nM = pl.ZERO - pl.NB, nk = pl.nk, NKP = pl.NKP;
+  const int VN = pl.DS + nk;  // construction-time image size
   auto region = [&](int d) { return (d >= pl.LX && d < pl.LX + nL) ? 0 : ((d >= pl.NB && d < pl.ZERO) ? 1 : -1); };
-  // read groups: (table, step, c, half) -> values
+  // read groups of the matrix operands: (table, step, c, half) -> values
   std::vector<std::vector<int>> groups;
-  std::vector<std::vector<int>> uses(pl.LDS_N);
+  std::vector<std::vector<int>> uses(VN);
   for (int w = 0; w < 2; ++w) {
     const auto& t = w ? pl.bwd : pl.fwd;
     const int ns = w ? pl.nbwd : pl.nfwd;
@@ -254,54 +263,86 @@ void layout_matrix_values(Plan& pl) {
         }
     }
   }
-  // capacity per (region, class)
-  int cap[2][32] = {};
-  const int rbase[2] = {pl.LX, pl.NB}, rsize[2] = {nL, nM};
-  for (int rg = 0; rg < 2; ++rg)
+  int nlive = 0;
+  for (int k = 0; k < nL; ++k) nlive += !uses[pl.LX + k].empty();
+  // final layout
+  const int pL = 0;
+  const int pW = pL + nlive, pC = pW + NKP;
+  const int endL = std::max(pL + nL, pC + NKP);
+  const int pDINV = endL, pNB = pDINV + NKP;
+  const int pZERO = pNB + nM;
+  int end = pZERO + 4;
+  const int pDS = (nM >= nk) ? pNB : end;
+  if (pDS == end) end += nk;
+  const bool pad_sinks = NKP - nk - 1 >= 32;
+  const int pSINK = pad_sinks ? -1 : end;
+  if (!pad_sinks) end += 64;
+  // ranges the class assignment distributes values over: L-live, L-dead, N | G | G'
+  const int rbase[3] = {pL, pL + nlive, pNB}, rsize[3] = {nlive, nL - nlive, nM};
+  auto sub = [&](int d) { return region(d) == 1 ? 2 : (uses[d].empty() ? 1 : 0); };
+  int cap[3][32] = {};
+  for (int rg = 0; rg < 3; ++rg)
     for (int k = 0; k < rsize[rg]; ++k) cap[rg][(rbase[rg] + k) % 32]++;
-  std::vector<int> cls(pl.LDS_N, -1);
-  // values without solve uses keep any class: first the constrained ones, biggest groups first
-  std::vector<int> order(groups.size());
-  for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return groups[a].size() > groups[b].size(); });
-  for (int gi : order) {
-    for (int d : groups[gi]) {
-      if (cls[d] >= 0) continue;
-      const int rg = region(d);
-      int best = -1, bestp = 1 << 30;
-      for (int c = 0; c < 32; ++c) {
-        if (cap[rg][c] == 0) continue;
-        int pen = 0;
-        for (int u : uses[d])
-          for (int o : groups[u])
-            if (o != d && cls[o] == c) pen++;
-        if (pen < bestp) bestp = pen, best = c;
+  std::vector<int> cls(VN, -1);
+  if (conflict_layout) {
+    std::vector<int> order(groups.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return groups[a].size() > groups[b].size(); });
+    for (int gi : order) {
+      for (int d : groups[gi]) {
+        if (cls[d] >= 0) continue;
+        const int rg = sub(d);
+        int best = -1, bestp = 1 << 30;
+        for (int c = 0; c < 32; ++c) {
+          if (cap[rg][c] == 0) continue;
+          int pen = 0;
+          for (int u : uses[d])
+            for (int o : groups[u])
+              if (o != d && cls[o] == c) pen++;
+          if (pen < bestp) bestp = pen, best = c;
+        }
+        cls[d] = best;
+        cap[rg][best]--;
       }
-      cls[d] = best;
-      cap[rg][best]--;
     }
   }
-  // slots per class, then the permutation
-  std::vector<int> perm(pl.LDS_N);
-  for (int d = 0; d < pl.LDS_N; ++d) perm[d] = d;
-  for (int rg = 0; rg < 2; ++rg) {
-    std::vector<std::vector<int>> free_slots(32);
-    for (int k = 0; k < rsize[rg]; ++k) free_slots[(rbase[rg] + k) % 32].push_back(rbase[rg] + k);
-    std::vector<size_t> next(32, 0);
-    std::vector<int> rest;
-    for (int k = 0; k < rsize[rg]; ++k) {
-      const int d = rbase[rg] + k;
-      if (cls[d] >= 0)
-        perm[d] = free_slots[cls[d]][next[cls[d]]++];
-      else
-        rest.push_back(d);
+  std::vector<int> rel(VN, -1);
+  {  // L and N | G | G': class-constrained values first, the others fill the remaining slots
+    std::vector<std::vector<int>> members(3);
+    for (int k = 0; k < nL; ++k) members[sub(pl.LX + k)].push_back(pl.LX + k);
+    for (int k = 0; k < nM; ++k) members[2].push_back(pl.NB + k);
+    for (int rg = 0; rg < 3; ++rg) {
+      std::vector<std::vector<int>> free_slots(32);
+      for (int k = 0; k < rsize[rg]; ++k) free_slots[(rbase[rg] + k) % 32].push_back(rbase[rg] + k);
+      std::vector<size_t> next(32, 0);
+      std::vector<int> rest;
+      for (int d : members[rg]) {
+        if (cls[d] >= 0)
+          rel[d] = free_slots[cls[d]][next[cls[d]]++];
+        else
+          rest.push_back(d);
+      }
+      std::vector<int> left;
+      for (int c = 0; c < 32; ++c)
+        for (size_t i = next[c]; i < free_slots[c].size(); ++i) left.push_back(free_slots[c][i]);
+      for (size_t i = 0; i < rest.size(); ++i) rel[rest[i]] = left[i];
     }
-    std::vector<int> left;
-    for (int c = 0; c < 32; ++c)
-      for (size_t i = next[c]; i < free_slots[c].size(); ++i) left.push_back(free_slots[c][i]);
-    for (size_t i = 0; i < rest.size(); ++i) perm[rest[i]] = left[i];
   }
-  auto mp = [&](uint32_t byteaddr) { return (uint32_t)perm[byteaddr / 8u] * 8u; };
+  for (int k = 0; k < NKP; ++k) {
+    rel[pl.DINV + k] = pDINV + k;
+    rel[pl.W + k] = pW + k;
+    rel[pl.CACC + k] = pC + k;
+  }
+  for (int k = 0; k < 4; ++k) rel[pl.ZERO + k] = pZERO + k;
+  for (int l = 0; l < 64; ++l)  // lanes 0-31: W padding, 32-63: C padding (conflict-free groups)
+    rel[pl.SINK + l] = pad_sinks ? (l < 32 ? pW + nk + 1 + l : pC + nk + 1 + (l - 32)) : pSINK + l;
+  for (int j = 0; j < nk; ++j) rel[pl.DS + j] = pDS + j;
+  for (int d = 0; d < VN; ++d)
+    if (rel[d] < 0) {
+      fprintf(stderr, "mpcqp: internal: construction slot %d has no place in the LDS image\n", d);
+      abort();
+    }
+  auto mp = [&](uint32_t byteaddr) { return (uint32_t)rel[byteaddr / 8u] * 8u; };
   for (int w = 0; w < 2; ++w) {
     auto& t = w ? pl.bwd : pl.fwd;
     for (auto& x : t) x = mp(x);  // every solve word is a byte address
@@ -313,16 +354,25 @@ void layout_matrix_values(Plan& pl) {
       uint32_t* r = t.data() + (size_t)s * FAC_STEP_WORDS;
       for (int l = 0; l < 64; ++l) {
         const uint32_t tgt = r[l] & META_TGT_MASK;
-        if (tgt / 8u < (uint32_t)pl.LDS_N) r[l] = (r[l] & ~META_TGT_MASK) | mp(tgt);
+        if (r[l] & META_HEAD) r[l] = (r[l] & ~META_TGT_MASK) | mp(tgt);
       }
       for (int k = 64; k < FAC_STEP_WORDS; ++k) r[k] = mp(r[k]);
     }
   }
-  for (auto& x : pl.slotP) x = (uint16_t)perm[x];
-  for (auto& x : pl.slotA) x = (uint16_t)perm[x];
+  auto mp16 = [&](std::vector<uint16_t>& v) {
+    for (auto& x : v) x = (uint16_t)rel[x];
+  };
+  mp16(pl.slotP), mp16(pl.slotA), mp16(pl.slotRho), mp16(pl.slotSig), mp16(pl.wsx), mp16(pl.wsz);
   std::vector<uint16_t> lc(nL);
-  for (int k = 0; k < nL; ++k) lc[perm[pl.LX + k] - pl.LX] = pl.Lcol[k];
+  for (int k = 0; k < nL; ++k) lc[rel[pl.LX + k] - pL] = (uint16_t)rel[pl.Lcol[k]];
   pl.Lcol.swap(lc);
+  pl.nLlive = nlive;
+  pl.LX = pL, pl.W = pW, pl.CACC = pC, pl.DINV = pDINV, pl.NB = pNB;
+  pl.GB = pNB + (pl.GB - pl.NB), pl.GPB = pNB + (pl.GPB - pl.NB);  // region bounds (values permuted)
+  pl.ZERO = pZERO, pl.ONE = pZERO + 1, pl.MONE = pZERO + 2;
+  pl.DS = pDS;
+  pl.SINK = pad_sinks ? pW + nk + 1 : pSINK;
+  pl.LDS_N = end;
 }
 
 // padded per-slot ELL of `count` outputs; terms(e) lists (src, in) in summation order
@@ -393,7 +443,10 @@ void dump_conflicts(const Plan& pl) {
           for (int l = 16 * g; l < 16 * g + 16; ++l) {
             const uint32_t d = r[SOLVE_TERM_WORDS + l * 4 + q] / 8u;
             cnt[d % 16]++;
-            if (d < (uint32_t)pl.SINK || d >= (uint32_t)pl.SINK + 64) used++;
+            const bool sink = (d > (uint32_t)(pl.W + pl.nk) && d < (uint32_t)(pl.W + pl.NKP)) ||
+                              (d > (uint32_t)(pl.CACC + pl.nk) && d < (uint32_t)(pl.CACC + pl.NKP)) ||
+                              (d >= (uint32_t)pl.SINK && d < (uint32_t)pl.SINK + 64);
+            if (!sink) used++;
           }
           ct += *std::max_element(cnt, cnt + 16);
         }
@@ -673,8 +726,9 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   pl.ZERO = pl.GPB + pl.nGP;
   pl.ONE = pl.ZERO + 1;
   pl.MONE = pl.ZERO + 2;
-  pl.SINK = pl.ZERO + 4;    // 64 sink slots for idle lanes of solve steps
-  pl.LDS_N = pl.SINK + 64;  // keeps the image a multiple of 16 bytes with an even base
+  pl.SINK = pl.ZERO + 4;  // 64 sink slots for idle lanes of solve steps
+  pl.DS = pl.SINK + 64;   // D scratch of the factorization
+  pl.LDS_N = pl.DS + nk;  // construction-time image; relocate() lays out the final one
   // slot of N_{r r2} (r2 in reach(r) or r2 == r -> MONE), G_{r x}, G'_{r z}
   auto nslot = [&](int r, int r2) -> int {
     if (r2 == r) return pl.MONE;
@@ -690,13 +744,11 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     auto it = std::lower_bound(gppat[r].begin(), gppat[r].end(), z);
     return pl.GPB + gpoff[r] + (int)(it - gppat[r].begin());
   };
-  // scaling overlay
+  // scaling overlay (physical: from the image base, over whatever the final layout holds there)
   pl.S_P = 0;
   pl.S_A = pl.S_P + pl.nnzP;
   pl.S_DT = pl.S_A + pl.nnzA;
   pl.S_ET = pl.S_DT + n;
-  if (pl.S_ET + m > pl.LDS_N) pl.LDS_N = pl.S_ET + m;
-  pl.LDS_N = (pl.LDS_N + 1) & ~1;
   // the residual SpMVs stage x (n) and y (m) as plain arrays in the W + C regions
   if (pl.LDS_N * 8 > (int)META_TGT_MASK || pl.LDS_N >= 65535) {
     pl.error = "LDS image too large for the schedule's byte addresses";
@@ -706,12 +758,12 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   // ---- KKT assembly maps
   pl.slotP.resize(pl.nnzP);
   pl.slotSig.resize(n);
-  for (int j = 0; j < n; j++) pl.slotSig[j] = (uint16_t)(pl.W + pl.pinv[j]);
+  for (int j = 0; j < n; j++) pl.slotSig[j] = (uint16_t)(pl.DS + pl.pinv[j]);
   for (int j = 0; j < n; j++)
     for (int p = Pp[j]; p < Pp[j + 1]; p++) {
       int i = Pi[p];
       if (i == j) {
-        pl.slotP[p] = (uint16_t)(pl.W + pl.pinv[j]);
+        pl.slotP[p] = (uint16_t)(pl.DS + pl.pinv[j]);
       } else {
         int a = pl.pinv[i], b = pl.pinv[j];
         int pos = lpos(std::max(a, b), std::min(a, b));
@@ -734,7 +786,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
       pl.slotA[p] = (uint16_t)(pl.LX + pos);
     }
   pl.slotRho.resize(m);
-  for (int i = 0; i < m; i++) pl.slotRho[i] = (uint16_t)(pl.W + pl.pinv[n + i]);
+  for (int i = 0; i < m; i++) pl.slotRho[i] = (uint16_t)(pl.DS + pl.pinv[n + i]);
   pl.wsx.resize(n);
   pl.wsz.resize(m);
   for (int i = 0; i < n; i++) pl.wsx[i] = (uint16_t)(pl.W + pl.pinv[i]);
@@ -758,7 +810,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     std::vector<Task> tasks;
     for (int j : bylev[L]) {
       Task d;
-      d.target = pl.W + j;
+      d.target = pl.DS + j;
       d.isD = true;
       d.inplace = true;
       for (int k : lrow[j]) {
@@ -899,8 +951,10 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   }
   pl.levels_fwd = T;
   pl.levels_bwd = T;
-  if (!getenv("MPCQP_NO_LAYOUT")) layout_matrix_values(pl);
+  relocate(pl, !getenv("MPCQP_NO_LAYOUT"));
   if (getenv("MPCQP_DUMP_CONFLICTS")) dump_conflicts(pl);
+  if (pl.S_ET + m > pl.LDS_N) pl.LDS_N = pl.S_ET + m;  // the scaling value overlay
+  pl.LDS_N = (pl.LDS_N + 1) & ~1;
 
   // ---- matrix structure for scaling / residuals
   pl.Ap.resize(n + 1);

@@ -82,15 +82,23 @@ inline bool kernel_bucket(int n, int m, int& rn, int& rm) {
 struct Plan {
   int n = 0, m = 0, nk = 0, nnzP = 0, nnzA = 0, nnzL = 0;
   std::vector<int32_t> perm, pinv, Lp, Li, etree;
-  // LDS layout, in doubles: L | 1/D | W (solve vector) | C (accumulators) | N (negated block
-  // inverses) | G | G' | ZERO ONE MONE pad | SINK (64 slots)
+  // LDS layout, in doubles, phase by phase over one image (relocate() in symbolic.cpp):
+  //   [ L (nnzL): the solve-live entries first, then the entries the solves never read ]
+  //       W (solve vector) and C (accumulators) overlay the solve-dead L entries: they are only
+  //       used between factorizations, and the factorization rewrites all of L
+  //   [ 1/D ]  [ N (negated block inverses) | G | G' ]  [ ZERO ONE MONE pad ]
+  //       the D scratch of the factorization (the KKT diagonal, then D) overlays N: N, G, G' are
+  //       written by the factorization tail, after D is no longer read
+  //   the solve steps' sink slots (targets of unused segments) sit in the W and C padding
   int LX = 0, DINV = 0, W = 0, CACC = 0, NB = 0, GB = 0, GPB = 0, ZERO = 0, ONE = 0, MONE = 0;
+  int DS = 0;      // D scratch of the factorization (nk doubles)
+  int nLlive = 0;  // L entries the solves read (far-block couplings)
   // the 1/D, W and C regions are NKP = 64 * (RN + RM) doubles long (the kernel's register-slot bucket,
   // kernel_bucket below): whole 64-lane slots, so the per-iteration vector passes store
   // unconditionally, and slot nk of each (the "junk" slot) takes the stores of lanes past the end of x
   // or z (W[nk] is zeroed every iteration and read back as 0)
   int NKP = 0;
-  int SINK = 0;
+  int SINK = 0;   // construction-time base of the 64 sink slots (relocated per lane)
   int LDS_N = 0;
   // blocked substitution: contiguous blocks of the permuted order
   std::vector<int32_t> block_start;  // T + 1 entries
