@@ -161,6 +161,16 @@ int mpcqp_engine_kind(const mpcqp_handle *h, int32_t *kind);
  * {fac_steps, fwd_steps, bwd_steps, fwd_levels, bwd_levels, lds_image_bytes}. */
 int mpcqp_analyze(const mpcqp_structure *st, int32_t *perm, int32_t *Lp, int32_t *Li,
                   int32_t *nnzL, int32_t *stats);
+/* Host-only schedule self-check (no HIP call): compiles the same plan mpcqp_create would and
+ * interprets it on the CPU for one instance -- KKT assembly from Px (upper CSC of P), Ax (CSC of A),
+ * sigma and rho_vec [m], the factorization schedule, then one forward / diagonal / backward solve
+ * of [[P + sigma I, A'], [A, -diag(1/rho_vec)]] sol = rhs (sol, rhs [n+m], host arrays).  model
+ * [4] (may be NULL) receives the modelled LDS cycles of one ADMM iteration's solve work for one
+ * wave: solve-step reads, solve-step atomics, vector passes, and the conflict-free floor of the
+ * same instructions.  Diagnostics / tests only; the product path never calls it. */
+int mpcqp_schedule_check(const mpcqp_structure *st, const double *Px, const double *Ax,
+                         double sigma, const double *rho_vec, const double *rhs, double *sol,
+                         int64_t *model);
 /* Host-side export of the symbolic analysis for white-box tests (no device work):
  * perm [n+m] (KKT position -> original KKT index), Lp [n+m+1], Li [nnzL]. */
 int mpcqp_export_symbolic(const mpcqp_handle *h, int32_t *perm, int32_t *Lp, int32_t *Li);

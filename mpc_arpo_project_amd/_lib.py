@@ -19,6 +19,7 @@ EXPORTED = (
     "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",
     "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
     "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_get_state", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
+    "mpcqp_schedule_check",
     "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind",
     "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
     "mpcqp_cl_set_ids", "mpcqp_cl_set_tracking", "mpcqp_cl_noise", "mpcqp_cl_set_plant", "mpcqp_clc_period",
@@ -121,6 +122,8 @@ def lib():
     L.mpcqp_schedule_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
     L.mpcqp_export_symbolic.argtypes = [vp, i32p, i32p, i32p]
     L.mpcqp_analyze.argtypes = [C.POINTER(Structure), i32p, i32p, i32p, i32p, i32p]
+    L.mpcqp_schedule_check.argtypes = [C.POINTER(Structure), dp, dp, C.c_double, dp, dp, dp,
+                                       C.POINTER(C.c_int64)]
     L.mpcqp_cl_create.argtypes = [C.POINTER(ClScenario), i32, vp, C.POINTER(vp)]
     L.mpcqp_cl_destroy.argtypes = [vp]
     L.mpcqp_cl_configure.argtypes = [vp, dp, dp, dp, dp]
@@ -190,3 +193,31 @@ def analyze(P_triu_csc, A_csc):
           "mpcqp_analyze")
     keys = ("fac_steps", "fwd_steps", "bwd_steps", "fwd_levels", "bwd_levels", "lds_image_bytes")
     return perm, Lp, Li[:nnz.value], dict(zip(keys, stats.tolist()))
+
+
+def schedule_check(P_triu_csc, A_csc, sigma, rho_vec, rhs):
+    """Host-only (no GPU): the compiled device program interpreted on the CPU for one instance
+    (assembly, factorization, one KKT solve).  Returns (solution of the KKT system for rhs,
+    modelled LDS cycles dict).  Test / diagnostic use."""
+    import numpy as np
+
+    n, m = P_triu_csc.shape[0], A_csc.shape[0]
+    Pp = np.ascontiguousarray(P_triu_csc.indptr, dtype=np.int32)
+    Pi = np.ascontiguousarray(P_triu_csc.indices, dtype=np.int32)
+    Ap = np.ascontiguousarray(A_csc.indptr, dtype=np.int32)
+    Ai = np.ascontiguousarray(A_csc.indices, dtype=np.int32)
+    i32 = C.POINTER(C.c_int32)
+    d = C.POINTER(C.c_double)
+    st = Structure(n, m, Pp.ctypes.data_as(i32), Pi.ctypes.data_as(i32), Ap.ctypes.data_as(i32),
+                   Ai.ctypes.data_as(i32))
+    Px = np.ascontiguousarray(P_triu_csc.data, dtype=np.float64)
+    Ax = np.ascontiguousarray(A_csc.data, dtype=np.float64)
+    rho = np.ascontiguousarray(rho_vec, dtype=np.float64)
+    b = np.ascontiguousarray(rhs, dtype=np.float64)
+    sol = np.empty(n + m, dtype=np.float64)
+    model = np.zeros(4, dtype=np.int64)
+    check(lib().mpcqp_schedule_check(C.byref(st), Px.ctypes.data_as(d), Ax.ctypes.data_as(d),
+                                     float(sigma), rho.ctypes.data_as(d), b.ctypes.data_as(d),
+                                     sol.ctypes.data_as(d), model.ctypes.data_as(C.POINTER(C.c_int64))),
+          "mpcqp_schedule_check")
+    return sol, dict(zip(("read", "atomic", "vec", "floor"), model.tolist()))

@@ -58,7 +58,6 @@ struct DevPlan {
   const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
   int n, m, nk, nnzP, nnzA, nnzL;
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
-  int DS;  // D scratch of the factorization (overlays the block-inverse region)
   int NKS;  // 64-lane slots of the padded 1/D, W and C regions (symbolic.hpp NKP / 64 = RN + RM)
   // scaling index overlay (symbolic.hpp): 16-byte chunks copied to LDS at u16 offset SCI
   const uint4* sci_src;
@@ -269,6 +268,15 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
   lds_st(v, r.t1, n1);
   lds_st(v, r.t2, n2);
   lds_st(v, r.t3, n3);
+#elif defined(EXP_NO_ATOMIC)  // timing ablation: no LDS writes at all (keeps the values live)
+  asm volatile("" ::"v"(n0), "v"(n1), "v"(n2), "v"(n3));
+#elif defined(EXP_MASKED_ADDS)  // timing ablation: atomics 1-3 issued with EXP_MASKED_ADDS lanes
+  lds_add(r.t0, n0);
+  if (__lane_id() < EXP_MASKED_ADDS) {
+    lds_add(r.t1, n1);
+    lds_add(r.t2, n2);
+    lds_add(r.t3, n3);
+  }
 #elif defined(EXP_TWO_ADDS)  // timing ablation: two atomics per lane
   lds_add(r.t0, n0 + n1);
   lds_add(r.t2, n2 + n3);
@@ -280,9 +288,10 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
 #endif
   LDS_FENCE();
 }
-// One factorization step: v[t] <- -sum_c v[a_c] v[b_c] v[c_c]; a D_j target also writes 1/D_j at
-// byte offset dshift from it.  Only group heads store (idle lanes have no slot).
-__device__ __forceinline__ void fac_step(const FacRec& r, double* v, uint32_t dshift) {
+// One factorization step: v[t] <- -sum_c v[a_c] v[b_c] v[c_c]; a D_j task (in place on the 1/D slot,
+// which holds the KKT diagonal until then) stores 1/D_j instead.  Only group heads store (idle
+// lanes have no slot).
+__device__ __forceinline__ void fac_step(const FacRec& r, double* v) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(r.mt);
   const uint32_t C = (m0 >> META_C_SHIFT) & 15u, glog = (m0 >> META_SGLOG_SHIFT) & 7u;
   double acc = C <= 2 ? dot3<2>(v, r) : dot3<4>(v, r);
@@ -290,8 +299,7 @@ __device__ __forceinline__ void fac_step(const FacRec& r, double* v, uint32_t ds
   if (r.mt & META_HEAD) {
     const uint32_t t = r.mt & META_TGT_MASK;
     const double nv = -acc;
-    lds_st(v, t, nv);
-    if (r.mt & META_ISD) lds_st(v, t + dshift, 1.0 / nv);
+    lds_st(v, t, (r.mt & META_ISD) ? 1.0 / nv : nv);
   }
   LDS_FENCE();
 }
@@ -362,30 +370,27 @@ struct FacOps {
   typedef FacRec Rec;
   static constexpr int STRIDE = FAC_STEP_WORDS;
   double* v;
-  uint32_t dshift;
   __device__ __forceinline__ static void load(Rsrc rs, int soff, uint32_t lane, Rec& r) {
     load_fac(rs, soff, lane, r);
   }
-  __device__ __forceinline__ void step(const Rec& r, int) const { fac_step(r, v, dshift); }
+  __device__ __forceinline__ void step(const Rec& r, int) const { fac_step(r, v); }
 };
-__device__ __forceinline__ void run_fac(const uint32_t* tbl, int nsteps, double* v, int lane,
-                                        uint32_t dshift) {
+__device__ __forceinline__ void run_fac(const uint32_t* tbl, int nsteps, double* v, int lane) {
   Pipe<FacOps> pp;
   const Rsrc rs = table_rsrc(tbl, nsteps, FAC_STEP_WORDS);
   prefetch(rs, nsteps, (uint32_t)lane, pp);
-  run_body(rs, nsteps, (uint32_t)lane, FacOps{v, dshift}, pp);
+  run_body(rs, nsteps, (uint32_t)lane, FacOps{v}, pp);
 }
 
 // numeric LDL': U = L D and D by levels, L = U / D (flat pass), then the block-inverse tail
 __device__ __forceinline__ void run_factor(const KParams& p, double* v, int lane) {
   const DevPlan& P = p.pl;
-  const uint32_t dshift = (uint32_t)(P.DINV - P.DS) * 8u;  // may wrap: DINV precedes DS
-  run_fac(P.fac, P.nfac, v, lane, dshift);
+  run_fac(P.fac, P.nfac, v, lane);
   LDS_FENCE();
 #pragma unroll 4
   for (int k = lane; k < P.nnzL; k += 64) v[P.LX + k] *= v[P.Lcol[k]];
   LDS_FENCE();
-  if (P.ntail > 0) run_fac(P.tail, P.ntail, v, lane, dshift);
+  if (P.ntail > 0) run_fac(P.tail, P.ntail, v, lane);
 }
 
 // constraint classes packed 2 bits per register slot (auxil.c constr_type)
@@ -612,9 +617,12 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
                                     const Inst<RN, RM>& S) {
   const DevPlan& P = p.pl;
   for (int k = lane; k < P.nnzL; k += 64) v[P.LX + k] = 0.0;
-  for (int k = lane; k < P.nk; k += 64) v[P.DS + k] = 0.0;
+  // the whole 1/D region (the D_j tasks' KKT diagonal in, 1/D_j out; 0 in the padding, which the
+  // diagonal pass multiplies with the zeroed W padding)
+#pragma unroll
+  for (int r = 0; r < RN + RM; ++r) v[P.DINV + lane + 64 * r] = 0.0;
+  if (lane < ZERO_BLOCK) v[P.ZERO + lane] = 0.0;
   if (lane == 0) {
-    v[P.ZERO] = 0.0;
     v[P.ONE] = 1.0;
     v[P.MONE] = -1.0;
   }
@@ -1068,18 +1076,13 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   S.pri_res = S.dua_res = 0.0;
 
   // ---------------- ADMM (osqp.c osqp_solve)
-  // LDS slots of this lane's x / z entries in the permuted solve vector (kept in registers)
+  // LDS slots of this lane's x / z entries in the permuted solve vector (kept in registers); lanes
+  // past the end of x or z have their own W padding slot, zeroed every iteration and read back as 0
   int wsx[RN], wsz[RM];
 #pragma unroll
-  for (int r = 0; r < RN; ++r) {
-    const int j = lane + 64 * r;
-    wsx[r] = j < n ? (int)P.wsx[j] : P.W + P.nk;  // junk slot
-  }
+  for (int r = 0; r < RN; ++r) wsx[r] = (int)P.wsx[lane + 64 * r];
 #pragma unroll
-  for (int r = 0; r < RM; ++r) {
-    const int i = lane + 64 * r;
-    wsz[r] = i < m ? (int)P.wsz[i] : P.W + P.nk;
-  }
+  for (int r = 0; r < RM; ++r) wsz[r] = (int)P.wsz[lane + 64 * r];
   const int coff = P.CACC - P.W;  // rhs goes to the accumulator region, the solution comes back in W
   // loop constants held in VGPRs (an opaque copy: otherwise they are re-read from the kernel
   // arguments inside the loop, with an lgkmcnt(0) wait that also drains the LDS queue)
@@ -1540,7 +1543,6 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.nnzL = pl.nnzL;
     dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.CACC = pl.CACC, dp.ZERO = pl.ZERO;
     dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N, dp.NKS = pl.NKP / 64;
-    dp.DS = pl.DS;
     dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
     dp.sci_src = (const uint4*)(b + o_sci), dp.SCI = pl.SCI, dp.S_ZERO = pl.S_ZERO;
     dp.sci_n16 = (int)(pl.sci_block.size() / 8);
@@ -1779,6 +1781,22 @@ int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t
     stats[4] = pl.levels_bwd;
     stats[5] = pl.LDS_N * (int)sizeof(double);
   }
+  return 0;
+}
+
+int mpcqp_schedule_check(const mpcqp_structure* st, const double* Px, const double* Ax,
+                         double sigma, const double* rho_vec, const double* rhs, double* sol,
+                         int64_t* model) {
+  if (!st || !Px || !Ax || !rho_vec || !rhs || !sol) return fail(MPCQP_E_INVALID, "null argument");
+  Plan pl;
+  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w()))
+    return fail(MPCQP_E_UNSUPPORTED, pl.error);
+  if (model) {
+    const LdsModel md = model_lds(pl);
+    model[0] = md.read, model[1] = md.atomic, model[2] = md.vec, model[3] = md.floor;
+  }
+  if (!emulate_kkt_solve(pl, Px, Ax, sigma, rho_vec, rhs, sol))
+    return fail(MPCQP_E_INVALID, "schedule emulation produced a non-finite or unzeroed slot");
   return 0;
 }
 

@@ -241,7 +241,7 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
 //     both solves get the class that collides least).
 void relocate(Plan& pl, bool conflict_layout) {
   const int nL = pl.nnzL, nM = pl.ZERO - pl.NB, nk = pl.nk, NKP = pl.NKP;
-  const int VN = pl.DS + nk;  // construction-time image size
+  const int VN = pl.SINK + 64;  // construction-time image size
   auto region = [&](int d) { return (d >= pl.LX && d < pl.LX + nL) ? 0 : ((d >= pl.NB && d < pl.ZERO) ? 1 : -1); };
   // read groups of the matrix operands: (table, step, c, half) -> values
   std::vector<std::vector<int>> groups;
@@ -271,9 +271,7 @@ void relocate(Plan& pl, bool conflict_layout) {
   const int endL = std::max(pL + nL, pC + NKP);
   const int pDINV = endL, pNB = pDINV + NKP;
   const int pZERO = pNB + nM;
-  int end = pZERO + 4;
-  const int pDS = (nM >= nk) ? pNB : end;
-  if (pDS == end) end += nk;
+  int end = pZERO + CONST_SLOTS;
   const bool pad_sinks = NKP - nk - 1 >= 32;
   const int pSINK = pad_sinks ? -1 : end;
   if (!pad_sinks) end += 64;
@@ -333,10 +331,9 @@ void relocate(Plan& pl, bool conflict_layout) {
     rel[pl.W + k] = pW + k;
     rel[pl.CACC + k] = pC + k;
   }
-  for (int k = 0; k < 4; ++k) rel[pl.ZERO + k] = pZERO + k;
+  for (int k = 0; k < CONST_SLOTS; ++k) rel[pl.ZERO + k] = pZERO + k;
   for (int l = 0; l < 64; ++l)  // lanes 0-31: W padding, 32-63: C padding (conflict-free groups)
     rel[pl.SINK + l] = pad_sinks ? (l < 32 ? pW + nk + 1 + l : pC + nk + 1 + (l - 32)) : pSINK + l;
-  for (int j = 0; j < nk; ++j) rel[pl.DS + j] = pDS + j;
   for (int d = 0; d < VN; ++d)
     if (rel[d] < 0) {
       fprintf(stderr, "mpcqp: internal: construction slot %d has no place in the LDS image\n", d);
@@ -369,8 +366,8 @@ void relocate(Plan& pl, bool conflict_layout) {
   pl.nLlive = nlive;
   pl.LX = pL, pl.W = pW, pl.CACC = pC, pl.DINV = pDINV, pl.NB = pNB;
   pl.GB = pNB + (pl.GB - pl.NB), pl.GPB = pNB + (pl.GPB - pl.NB);  // region bounds (values permuted)
-  pl.ZERO = pZERO, pl.ONE = pZERO + 1, pl.MONE = pZERO + 2;
-  pl.DS = pDS;
+  pl.ZERO = pZERO, pl.ONE = pZERO + ZERO_BLOCK, pl.MONE = pZERO + ZERO_BLOCK + 1;
+  pl.DS = pDINV;
   pl.SINK = pad_sinks ? pW + nk + 1 : pSINK;
   pl.LDS_N = end;
 }
@@ -709,6 +706,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
       return false;
     }
     pl.NKP = 64 * (rn + rm);
+    pl.RN = rn, pl.RM = rm;
   }
   pl.DINV = pl.nnzL;
   pl.W = pl.DINV + pl.NKP;
@@ -723,12 +721,14 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   pl.nN = noff[nk], pl.nG = goff[nk], pl.nGP = gpoff[nk];
   pl.GB = pl.NB + pl.nN;
   pl.GPB = pl.GB + pl.nG;
-  pl.ZERO = pl.GPB + pl.nGP;
-  pl.ONE = pl.ZERO + 1;
-  pl.MONE = pl.ZERO + 2;
-  pl.SINK = pl.ZERO + 4;  // 64 sink slots for idle lanes of solve steps
-  pl.DS = pl.SINK + 64;   // D scratch of the factorization
-  pl.LDS_N = pl.DS + nk;  // construction-time image; relocate() lays out the final one
+  pl.ZERO = pl.GPB + pl.nGP;  // ZERO_BLOCK zero slots (one per read bank), then ONE, MONE
+  pl.ONE = pl.ZERO + ZERO_BLOCK;
+  pl.MONE = pl.ONE + 1;
+  pl.SINK = pl.ZERO + CONST_SLOTS;  // 64 sink slots for idle lanes of solve steps
+  // the factorization's D_j tasks run in place on the 1/D slot: the slot holds the KKT diagonal
+  // until the task replaces it with 1/D_j (no separate D scratch)
+  pl.DS = pl.DINV;
+  pl.LDS_N = pl.SINK + 64;  // construction-time image; relocate() lays out the final one
   // slot of N_{r r2} (r2 in reach(r) or r2 == r -> MONE), G_{r x}, G'_{r z}
   auto nslot = [&](int r, int r2) -> int {
     if (r2 == r) return pl.MONE;
@@ -787,10 +787,15 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     }
   pl.slotRho.resize(m);
   for (int i = 0; i < m; i++) pl.slotRho[i] = (uint16_t)(pl.DS + pl.pinv[n + i]);
-  pl.wsx.resize(n);
-  pl.wsz.resize(m);
-  for (int i = 0; i < n; i++) pl.wsx[i] = (uint16_t)(pl.W + pl.pinv[i]);
-  for (int i = 0; i < m; i++) pl.wsz[i] = (uint16_t)(pl.W + pl.pinv[n + i]);
+  // every lane of the kernel's register slots gets its own W slot: the padding lanes past n (x) and
+  // past m (z) take the NKP - nk padding slots, so the vector passes need no lane masks and no two
+  // lanes share an address
+  pl.wsx.resize(64 * pl.RN);
+  pl.wsz.resize(64 * pl.RM);
+  for (int i = 0; i < 64 * pl.RN; i++)
+    pl.wsx[i] = (uint16_t)(pl.W + (i < n ? pl.pinv[i] : nk + (i - n)));
+  for (int i = 0; i < 64 * pl.RM; i++)
+    pl.wsz[i] = (uint16_t)(pl.W + (i < m ? pl.pinv[n + i] : nk + (64 * pl.RN - n) + (i - m)));
 
   // ---- levels
   std::vector<int> lev(nk, 0), blev(nk, 0);
@@ -1066,21 +1071,31 @@ namespace mpcqp {
 bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                       const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu,
                       int max_per_cu) {
-  if (capM > 0 && capW > 0) return build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW);
+  // the LDS layout optimiser runs on the chosen plan (MPCQP_NO_ANNEAL=1: off, diagnostics)
+  const bool anneal = !getenv("MPCQP_NO_ANNEAL") && !getenv("MPCQP_NO_LAYOUT");
+  if (capM > 0 && capW > 0) {
+    if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW)) return false;
+    if (anneal) optimize_lds(plan);
+    return true;
+  }
   if (n <= 0 || m < 0) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);
   // structure key
   std::vector<int32_t> key;
   key.push_back(n), key.push_back(m), key.push_back(lds_per_cu), key.push_back(max_per_cu);
+  key.push_back(anneal);
   key.insert(key.end(), Pp, Pp + n + 1);
   key.insert(key.end(), Pi, Pi + Pp[n]);
   key.insert(key.end(), Ap, Ap + n + 1);
   key.insert(key.end(), Ai, Ai + Ap[n]);
   static std::mutex mu;
-  static std::map<std::vector<int32_t>, std::pair<int, int>> memo;
+  static std::map<std::vector<int32_t>, Plan> memo;  // final (optimised) plan per structure
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = memo.find(key);
-    if (it != memo.end()) return build_plan(n, m, Pp, Pi, Ap, Ai, plan, it->second.first, it->second.second);
+    if (it != memo.end()) {
+      plan = it->second;
+      return true;
+    }
   }
   static const int CM[] = {96, 112, 128, 144, 160, 176, 192, 224, 256};
   static const int CW[] = {320, 352, 384, 416, 448, 480};
@@ -1101,11 +1116,13 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
       }
     }
   if (!found) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);  // reports the error
+  if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw)) return false;
+  if (anneal) optimize_lds(plan);
   {
     std::lock_guard<std::mutex> g(mu);
-    memo[key] = {bm, bw};
+    memo[key] = plan;
   }
-  return build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw);
+  return true;
 }
 
 }  // namespace mpcqp

@@ -38,6 +38,12 @@ constexpr int FAC_STEP_WORDS = 64 + 64 * 4 * FAC_MAXC;
 constexpr int SOLVE_TERM_WORDS = 64 * 2 * SOLVE_MAXC;
 constexpr int SOLVE_STEP_WORDS = SOLVE_TERM_WORDS + 64 * 4;
 
+// constant slots behind N | G | G': ZERO_BLOCK zeros (one per ds_read_b64 bank class, so the
+// padding terms of a solve step can read a zero from a bank no real operand of the instruction
+// half uses), ONE, MONE, padding
+constexpr int ZERO_BLOCK = 32;
+constexpr int CONST_SLOTS = ZERO_BLOCK + 4;
+
 // meta word: per-lane fields, then the step-wide C and glog (identical in every lane)
 constexpr uint32_t META_TGT_MASK = 0x1ffffu;  // factorization: LDS byte address of the target
 constexpr int META_GLOG_SHIFT = 17;           // 3 bits: this lane's group size log2
@@ -86,12 +92,13 @@ struct Plan {
   //   [ L (nnzL): the solve-live entries first, then the entries the solves never read ]
   //       W (solve vector) and C (accumulators) overlay the solve-dead L entries: they are only
   //       used between factorizations, and the factorization rewrites all of L
-  //   [ 1/D ]  [ N (negated block inverses) | G | G' ]  [ ZERO ONE MONE pad ]
-  //       the D scratch of the factorization (the KKT diagonal, then D) overlays N: N, G, G' are
-  //       written by the factorization tail, after D is no longer read
-  //   the solve steps' sink slots (targets of unused segments) sit in the W and C padding
+  //   [ 1/D ]  [ N (negated block inverses) | G | G' ]  [ ZERO x ZERO_BLOCK, ONE, MONE, pad ]
+  //       the factorization's D_j tasks run in place on the 1/D slots (KKT diagonal in, 1/D_j out)
+  //   unused solve segments add -0.0 (an exact no-op) to a sink slot; the layout optimiser
+  //   (lds_layout.cpp) picks any slot of a free bank, the unoptimised layout the W / C padding
   int LX = 0, DINV = 0, W = 0, CACC = 0, NB = 0, GB = 0, GPB = 0, ZERO = 0, ONE = 0, MONE = 0;
-  int DS = 0;      // D scratch of the factorization (nk doubles)
+  int DS = 0;      // slot base of the D_j tasks' targets (== DINV)
+  int RN = 0, RM = 0;  // the kernel's register-slot bucket (kernel_bucket)
   int nLlive = 0;  // L entries the solves read (far-block couplings)
   // the 1/D, W and C regions are NKP = 64 * (RN + RM) doubles long (the kernel's register-slot bucket,
   // kernel_bucket below): whole 64-lane slots, so the per-iteration vector passes store
@@ -114,7 +121,8 @@ struct Plan {
   // KKT assembly: LDS slot of each P entry (diagonal -> D slot), A entry, rho diagonal,
   // sigma diagonal (D slot of x_j)
   std::vector<uint16_t> slotP, slotA, slotRho, slotSig;
-  // LDS slot (permuted position in the W region) of x_i and z_i
+  // LDS slot (permuted position in the W region) of x_i and z_i for every lane of the kernel's
+  // register slots (64 RN and 64 RM entries; padding lanes get the W padding slots)
   std::vector<uint16_t> wsx, wsz;
   // schedules (STEP_WORDS words per step): factorization of U = L D and D by levels, then
   // (after the flat pass L = U * (1/D)_col) the block-inverse tail; forward and backward solves
@@ -148,5 +156,31 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
 bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                       const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu = 163840,
                       int max_per_cu = 4);
+
+// ---- lds_layout.cpp: LDS bank-conflict model and optimiser of the solve steps
+// Modelled LDS cycles of one ADMM iteration's solve work for one wave (MI355X_MICROARCH.md, LDS):
+// every ds_read_b64 serves two 32-lane halves, one cycle per distinct address on the busiest bank
+// (double slot mod 32; equal addresses broadcast); every ds_add_f64 / ds_write_b64 serves four
+// 16-lane groups, one cycle per lane on the busiest bank (slot mod 16; equal addresses serialise).
+struct LdsModel {
+  long read = 0, atomic = 0, vec = 0;  // solve-step reads, solve-step atomics, vector passes
+  long floor = 0;                      // the same instructions without any conflict
+};
+LdsModel model_lds(const Plan& pl);
+// Rewrites the plan so the solve steps and the per-iteration vector passes conflict less: segments
+// move between positions of their step, terms swap operands or segments, unused segments get
+// sinks and zero slots in free banks, and the slots of the solve-read matrix values (within the
+// L-live and N | G | G' regions) and of the vector entries (W, C and 1/D together) are permuted.
+// Every change is a relabelling or a reordering of exact no-op / commutative work except the order
+// of the atomic additions into one target (rounding only).  Deterministic.
+void optimize_lds(Plan& pl);
+
+// ---- emulate.cpp: host interpretation of the device program (diagnostics and tests only)
+// One instance: KKT assembly from Px (upper CSC of P), Ax (CSC of A), sigma and rho_vec (m), the
+// factorization schedule, the flat pass, the tail, then one forward / diagonal / backward solve of
+// K [x; nu] = rhs (n + m, original order); writes sol (n + m).  Atomic additions are applied in
+// lane order (the device's order within one instruction may differ: rounding only).
+bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, double sigma,
+                       const double* rho_vec, const double* rhs, double* sol);
 
 }  // namespace mpcqp

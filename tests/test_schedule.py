@@ -1,0 +1,59 @@
+"""The compiled device program, checked on the CPU (no GPU): mpcqp_schedule_check interprets the
+exact schedules mpcqp_create uploads -- KKT assembly, factorization with its group butterflies,
+the block-inverse tail, one forward / diagonal / backward solve -- and the result must solve the
+KKT system [[P + sigma I, A'], [A, -diag(1/rho)]] (OSQP 0.6 kkt.c form_KKT, the system the
+reference's osqp solves every ADMM iteration).  This pins the symbolic compiler and the LDS layout
+optimiser (csrc/lds_layout.cpp): every slot relabelling, segment move, operand flip and sink they
+make must leave the solve exact to rounding.  The LDS cost model is checked to be below the
+unoptimised layout's."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from mpc_arpo_project_amd import _lib
+from mpc_arpo_project_amd.engine import sorted_csc, triu_csc
+
+
+def _kkt(P, A, sigma, rho):
+    n, m = P.shape[0], A.shape[0]
+    Pf = sp.csc_matrix(P)
+    return sp.bmat([[Pf + sigma * sp.eye(n), A.T], [A, -sp.diags(1.0 / rho)]], format="csc")
+
+
+@pytest.mark.parametrize("Nx,dv", [(20, False), (40, True)])
+def test_emulated_schedule_solves_kkt(Nx, dv):
+    from conftest import problem
+
+    prob = problem(Nx, dv)
+    P, A = triu_csc(prob.P), sorted_csc(prob.A)
+    rng = np.random.default_rng(Nx)
+    for trial in range(3):
+        # the bench's P, random A values on A's pattern, rho over the adaptive-rho range with
+        # OSQP's equality class (1e3 rho)
+        Ax = A.copy()
+        Ax.data = prob.A.tocsc().sorted_indices().data * (1 + 0.1 * rng.standard_normal(A.nnz))
+        rho = 10.0 ** rng.uniform(-3, 2, A.shape[0])
+        rho[: A.shape[0] // 4] *= 1e3
+        sigma = 1e-6
+        rhs = rng.standard_normal(P.shape[0] + A.shape[0])
+        sol, model = _lib.schedule_check(P, Ax, sigma, rho, rhs)
+        K = _kkt(P + sp.triu(P, 1).T, Ax, sigma, rho)
+        ref = sp.linalg.spsolve(K, rhs)
+        rel = np.abs(sol - ref).max() / np.abs(ref).max()
+        res = np.abs(K @ sol - rhs).max() / np.abs(rhs).max()
+        assert rel < 1e-8 and res < 1e-9, (trial, rel, res)
+
+
+def test_layout_optimiser_lowers_modelled_lds_cycles(monkeypatch):
+    """the annealed layout (default) models fewer LDS cycles than the greedy one it starts from"""
+    from conftest import problem
+
+    prob = problem(20, False)
+    P, A = triu_csc(prob.P), sorted_csc(prob.A)
+    args = (P, A, 1e-6, np.ones(A.shape[0]), np.ones(P.shape[0] + A.shape[0]))
+    _, opt = _lib.schedule_check(*args)
+    monkeypatch.setenv("MPCQP_NO_ANNEAL", "1")
+    _, greedy = _lib.schedule_check(*args)
+    tot = lambda d: d["read"] + d["atomic"] + d["vec"]
+    assert opt["floor"] == greedy["floor"] == 13 * 48 + 6 * 6
+    assert tot(opt) < 0.8 * tot(greedy), (opt, greedy)
