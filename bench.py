@@ -298,8 +298,11 @@ def main(argv=None):
     Sn = summ.cpu().numpy()
     kt_cold = np.array([a.elapsed_time(b) for a, b in cold_ev]) * 1e-3
     ci = cold_it.cpu().numpy()
+    metric = METRIC if (args.nx, args.dv) == (20, False) else (
+        f"MPC-QP solves/sec @ N={args.nx}{', impulsive delta-v' if args.dv else ''}, CW, "
+        f"batch={B}; ADMM iters to {args.eps:g}")
     out = {
-        "metric": METRIC,
+        "metric": metric,
         "value": world * B * K / elapsed,
         "unit": "solves/s",
         "n_gpus": world,

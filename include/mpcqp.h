@@ -144,6 +144,11 @@ int mpcqp_set_skip(mpcqp_handle *h, const int32_t *skip);
  * For white-box parity tests (the oracle's oqp_get_state counterpart). */
 int mpcqp_get_state(const mpcqp_handle *h, double *xs, double *zs, double *ys, double *rho,
                     int32_t *has_state);
+/* The reverse of mpcqp_get_state (device pointers, same layout): overwrite the warm-start state,
+ * e.g. with another solver's iterates.  White-box parity tests only (the oracle's oqp_set_state
+ * counterpart). */
+int mpcqp_set_state(mpcqp_handle *h, const double *xs, const double *zs, const double *ys,
+                    const double *rho, const int32_t *has_state);
 
 /* Introspection. */
 int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA,

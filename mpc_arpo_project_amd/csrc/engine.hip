@@ -1734,6 +1734,20 @@ int mpcqp_get_state(const mpcqp_handle* h, double* xs, double* zs, double* ys, d
   return 0;
 }
 
+int mpcqp_set_state(mpcqp_handle* h, const double* xs, const double* zs, const double* ys,
+                    const double* rho, const int32_t* has_state) {
+  if (!h || !xs || !zs || !ys || !rho || !has_state) return fail(MPCQP_E_INVALID, "null argument");
+  const size_t B = (size_t)h->B;
+  const Plan& pl = h->plan;
+  HIPCHK(hipMemcpyAsync(h->xs, xs, sizeof(double) * B * pl.n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->zs, zs, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->ys, ys, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->rho, rho, sizeof(double) * B, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->has_state, has_state, sizeof(int32_t) * B, hipMemcpyDeviceToDevice,
+                        h->stream));
+  return 0;
+}
+
 int mpcqp_dims(const mpcqp_handle* h, int32_t* n, int32_t* m, int32_t* nnzP, int32_t* nnzA,
                int32_t* nnzL) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");

@@ -184,6 +184,16 @@ class BatchQP:
                                          rho.data_ptr(), hs.data_ptr()), "mpcqp_get_state")
         return dict(x=xs, z=zs, y=ys, rho=rho, has_state=hs)
 
+    def set_state(self, x, z, y, rho, has_state):
+        """Overwrite the warm-start state (the reverse of get_state; white-box tests)."""
+        f = dict(dtype=torch.float64, device=self.device)
+        t = [torch.as_tensor(a, **f).contiguous() for a in (x, z, y, rho)]
+        hs = torch.as_tensor(has_state, dtype=torch.int32, device=self.device).contiguous()
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        check(_lib.lib().mpcqp_set_state(self._h, *(a.data_ptr() for a in t), hs.data_ptr()),
+              "mpcqp_set_state")
+        self._keep(state=(t, hs))
+
     def warm_start(self, x, y):
         x = self._batch_vec(x, self.n, "x")
         y = self._batch_vec(y, self.m, "y")

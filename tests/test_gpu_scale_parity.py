@@ -135,6 +135,7 @@ def test_warm_closed_loop_lockstep():
     cl = BatchClosedLoop(prob, X, eps_abs=eps, eps_rel=eps)
     solvers = []
     agree, fast_diff, n_fast = [], [], 0
+    stat_counts = {}
     for k in range(K):
         Ax, l, u = (t.cpu().numpy() for t in cl.qp.copy_data())
         stt = {key: v.cpu().numpy() for key, v in cl.qp.get_state().items()}
@@ -158,8 +159,11 @@ def test_warm_closed_loop_lockstep():
             fast_diff.append((k, int(b), int(sg[b]), int(ig[b]), int(so[b]), int(io[b])))
         n_fast += int(fast.sum())
         agree.append(float(np.mean(sg == so)))
+        for v_, c_ in zip(*np.unique(sg, return_counts=True)):
+            stat_counts[int(v_)] = stat_counts.get(int(v_), 0) + int(c_)
     cl.close()
     print("per-step status agreement", [round(a, 5) for a in agree])
+    print("engine status counts over the loop", stat_counts)
     print(f"solves both sides finish within {FAST} iterations: {n_fast}, disagreeing: "
           f"{len(fast_diff)} (step, chaser, gpu status/iter, oracle status/iter) {fast_diff[:8]}")
     # 1 flip in 2048 is 0.05 %: per step at most 1 %, over the loop at most 0.3 % (measured

@@ -24,7 +24,8 @@ def build(extra=()):
            "-DMPCQP_TIMING", *extra, os.path.join(csrc, "engine.hip"),
            os.path.join(csrc, "closed_loop.hip"),
            os.path.join(csrc, "estimation.hip"),
-           os.path.join(csrc, "symbolic.cpp"), "-o", LIB]
+           os.path.join(csrc, "symbolic.cpp"), os.path.join(csrc, "lds_layout.cpp"),
+           os.path.join(csrc, "emulate.cpp"), "-o", LIB]
     subprocess.check_call(cmd)
 
 
