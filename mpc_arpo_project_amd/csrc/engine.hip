@@ -61,7 +61,7 @@ struct DevPlan {
   int NKS;  // 64-lane slots of the padded 1/D, W and C regions (symbolic.hpp NKP / 64 = RN + RM)
   // scaling index overlay (symbolic.hpp): 16-byte chunks copied to LDS at u16 offset SCI
   const uint4* sci_src;
-  int SCI, S_ZERO, sci_n16, sci_eP, sci_eAt, sci_eA, sci_Pi, sci_Pc, sci_Ai, sci_Ac;
+  int SCI, S_ZERO, sci_n16, sci_eP, sci_eAt, sci_eA, sci_ra, sci_ca;
 };
 
 struct KParams {
@@ -87,15 +87,18 @@ struct KParams {
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
 // s_memtime deltas accumulated per wave in SGPRs, added to p.timing at the end of each instance.
-enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_V0, T_V1, T_V2, T_NSLOT };
+enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_V0, T_V1, T_V2, T_RS0, T_RS1, T_RS2, T_RS3, T_RS4, T_NSLOT };
 #ifdef MPCQP_TIMING
 #define T_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define T_END(slot, v) tacc[slot] += __builtin_amdgcn_s_memtime() - (v)
 #define T_COUNT(slot) tacc[slot] += 1
+// value dependency barrier: the timestamp after it waits for x
+#define TSYNC(x) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(x))
 #else
 #define T_BEGIN(v)
 #define T_END(slot, v)
 #define T_COUNT(slot)
+#define TSYNC(x)
 #endif
 
 // Ordering between dependent wave-synchronous LDS phases.  A wave's LDS instructions are executed
@@ -445,8 +448,16 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       const int t = e.off[r] + 64 * k + lane;
+#ifdef EXP_NOVAL  // timing experiment: no value loads
+      a[r][k] = 1e-3 * (k + 1);
+#else
       a[r][k] = val[t];
+#endif
+#ifdef EXP_NOIDX  // timing experiment: no index loads
+      ix[r][k] = (uint32_t)((lane + 7 * k) & 63);
+#else
       ix[r][k] = e.in[t];
+#endif
     }
   }
 #pragma unroll
@@ -509,29 +520,33 @@ __device__ __forceinline__ void ell_absmax(const EllDev& e, const uint16_t* src,
       if (o == lane + 64 * r) out[r] = mx;
   }
 }
-// v[base + k] = (v[base + k] * v[oa + ia[k]]) * v[ob + ib[k]] for k < cnt (Ruiz rescale of the
-// matrix values), 8 elements per lane in flight
-__device__ __forceinline__ void scale_vals(double* v, int base, int cnt, const uint16_t* ia,
-                                           const uint16_t* ib, int oa, int ob, int lane) {
-  constexpr int U = 8;
+// Ruiz rescale of the value overlay [P | A] (cnt = nnzP + nnzA values from S_P):
+//   v[S_P + k] = ((v[S_P + k] * f) * v[ra[k]]) * v[ca[k]],  f = cp for P's values, 1 for A's
+// -- scaling.c's mat_premult_diag / mat_postmult_diag, with the previous pass's cost factor c
+// (mat_mult_scalar on P) deferred into this pass: the same multiplications in the same order, and
+// x * 1.0 is exact.  All index reads of a batch, then all value reads, then the stores.
+__device__ __forceinline__ void scale_pa(double* v, int S_P, int nnzP, int cnt, const uint16_t* ra,
+                                         const uint16_t* ca, double cp, int lane) {
+  constexpr int U = 16;
   for (int k0 = 0; k0 < cnt; k0 += 64 * U) {
     uint32_t a[U], b[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = k0 + 64 * u + lane, kc = k < cnt ? k : 0;
-      a[u] = ia[kc];
-      b[u] = ib[kc];
+      a[u] = ra[kc];
+      b[u] = ca[kc];
     }
     double x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = k0 + 64 * u + lane, kc = k < cnt ? k : 0;
-      x[u] = (v[base + kc] * v[oa + a[u]]) * v[ob + b[u]];
+      const double f = k < nnzP ? cp : 1.0;
+      x[u] = ((v[S_P + kc] * f) * v[a[u]]) * v[b[u]];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = k0 + 64 * u + lane;
-      if (k < cnt) v[base + k] = x[u];
+      if (k < cnt) v[S_P + k] = x[u];
     }
   }
 }
@@ -647,13 +662,21 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
 
 // update_info: scaled Ax, Px, A'y and the unscaled residual norms (auxil.c compute_pri_res /
 // compute_dua_res).  x and y are staged as plain arrays in the W region.
+#ifdef MPCQP_TIMING
+#define TACC_PARAM , unsigned long long* tacc
+#define TACC_ARG , tacc
+#else
+#define TACC_PARAM
+#define TACC_ARG
+#endif
 template <int RN, int RM>
 __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>& S, Resid<RN, RM>& R,
-                                  const Slab& sb, double* v, int lane) {
+                                  const Slab& sb, double* v, int lane TACC_PARAM) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
   double* xb = v + P.W;
   double* yb = v + P.W + n;
+  T_BEGIN(t_r0);
   LDS_FENCE();
   // unconditional stores: x's slots past n land in y's range and are overwritten by the y stores
   // that follow (a wave's LDS stores complete in order); y's slots past m stay inside the padded
@@ -665,9 +688,25 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   for (int r = 0; r < RM; ++r) yb[lane + 64 * r] = S.y[r];
   LDS_FENCE();
   double pr = 0.0, dr = 0.0;
-  ell_mv<RM, ELL_KA>(P.eA, sb.vA, xb, R.Ax, lane);  // padding terms are 0 * x
-  ell_mv<RN, ELL_KP>(P.eP, sb.vP, xb, R.Px, lane);
-  ell_mv<RN, ELL_KAT>(P.eAt, sb.vAt, yb, R.Aty, lane);
+#ifdef EXP_SLAB0  // timing experiment: every wave reads wave 0's (L2-resident) matrix values
+  const Slab sbv = slab_of(P, p.scratch);
+#else
+  const Slab& sbv = sb;
+#endif
+  T_END(T_RS0, t_r0);
+  T_BEGIN(t_r1);
+  ell_mv<RM, ELL_KA>(P.eA, sbv.vA, xb, R.Ax, lane);  // padding terms are 0 * x
+  TSYNC(R.Ax[0]);
+  T_END(T_RS1, t_r1);
+  T_BEGIN(t_r2);
+  ell_mv<RN, ELL_KP>(P.eP, sbv.vP, xb, R.Px, lane);
+  TSYNC(R.Px[0]);
+  T_END(T_RS2, t_r2);
+  T_BEGIN(t_r3);
+  ell_mv<RN, ELL_KAT>(P.eAt, sbv.vAt, yb, R.Aty, lane);
+  TSYNC(R.Aty[0]);
+  T_END(T_RS3, t_r3);
+  T_BEGIN(t_r4);
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
@@ -682,6 +721,8 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   }
   S.pri_res = wave_max(pr);
   S.dua_res = S.cinv * wave_max(dr);
+  TSYNC(S.dua_res);
+  T_END(T_RS4, t_r4);
 }
 
 template <int RN, int RM>
@@ -904,15 +945,25 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
     E[r] = 1.0;
   }
   S.c = 1.0;
+  double cprev = 1.0;  // cost factor of the last pass, not yet applied to P's values
+  double dpc[RN];      // P's column norms before that factor (the cost normalisation's)
   LDS_FENCE();
 #ifdef EXP_SKIP_SCALE  // timing ablation: no Ruiz passes
   for (int it = 0; it < 0; ++it) {
 #else
   for (int it = 0; it < p.s.scaling; ++it) {
 #endif
-    // compute_inf_norm_cols_KKT: columns of [P A'; A 0] (P symmetric from its upper triangle)
+    // compute_inf_norm_cols_KKT: columns of [P A'; A 0] (P symmetric from its upper triangle).
+    // After the first pass P's column norms are the cost normalisation's norms times its factor
+    // c (still pending on P's values): max_k |c x_k| = c max_k |x_k| exactly, rounding being
+    // monotonic (c > 0)
     double dp[RN], da[RN], er[RM], dt[RN], et[RM];
-    ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dp, lane);
+    if (it == 0) {
+      ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dp, lane);
+    } else {
+#pragma unroll
+      for (int r = 0; r < RN; ++r) dp[r] = cprev * dpc[r];
+    }
     ell_absmax<RN, ELL_KAT>(P.eAt, ix + P.sci_eAt, v, da, lane);
     ell_absmax<RM, ELL_KA>(P.eA, ix + P.sci_eA, v, er, lane);
 #pragma unroll
@@ -930,8 +981,7 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
       if (i < m) v[P.S_ET + i] = et[r];
     }
     LDS_FENCE();
-    scale_vals(v, P.S_P, P.nnzP, ix + P.sci_Pi, ix + P.sci_Pc, P.S_DT, P.S_DT, lane);
-    scale_vals(v, P.S_A, P.nnzA, ix + P.sci_Ai, ix + P.sci_Ac, P.S_ET, P.S_DT, lane);
+    scale_pa(v, P.S_P, P.nnzP, P.nnzP + P.nnzA, ix + P.sci_ra, ix + P.sci_ca, cprev, lane);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       S.q[r] = dt[r] * S.q[r];
@@ -941,13 +991,13 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
     for (int r = 0; r < RM; ++r) E[r] = E[r] * et[r];
     LDS_FENCE();
     // cost normalization: mean of P's column norms, |q|_inf
-    ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dp, lane);
+    ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dpc, lane);
     double csum = 0.0, qmax = 0.0;
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const int j = lane + 64 * r;
       if (j < n) {
-        csum += dp[r];
+        csum += dpc[r];
         qmax = dmaxd(qmax, fabs(S.q[r]));
       }
     }
@@ -955,12 +1005,14 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
     const double inq = limit_scaling(wave_max(qmax));
     c_temp = limit_scaling(dmaxd(c_temp, inq));
     c_temp = 1. / c_temp;
-    for (int k = lane; k < P.nnzP; k += 64) v[P.S_P + k] = v[P.S_P + k] * c_temp;
+    cprev = c_temp;  // P *= c_temp: applied by the next rescale pass (or below, after the last)
 #pragma unroll
     for (int r = 0; r < RN; ++r) S.q[r] = S.q[r] * c_temp;
     S.c = S.c * c_temp;
     LDS_FENCE();
   }
+  for (int k = lane; k < P.nnzP; k += 64) v[P.S_P + k] = v[P.S_P + k] * cprev;
+  LDS_FENCE();
 }
 
 // end of scale_data: constraint classes, scaled bounds, D / E and the scaled matrices parked in
@@ -1199,7 +1251,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #ifndef EXP_NOCHECK
     if (can_check || adapt) {
       T_BEGIN(t_rs);
-      compute_residuals(p, S, R, sb, v, lane);
+      compute_residuals(p, S, R, sb, v, lane TACC_ARG);
       T_END(T_RESID, t_rs);
       T_COUNT(T_NCHK);
     }
@@ -1246,7 +1298,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   T_BEGIN(t_tl);
   if (!can_check) {
     iter = iter - 1;
-    compute_residuals(p, S, R, sb, v, lane);
+    compute_residuals(p, S, R, sb, v, lane TACC_ARG);
     status = check_termination(p, S, R, dy, dx, sb, v, lane, false);
     if (status == 0) status = MPCQP_UNSOLVED;
   }
@@ -1547,7 +1599,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.sci_src = (const uint4*)(b + o_sci), dp.SCI = pl.SCI, dp.S_ZERO = pl.S_ZERO;
     dp.sci_n16 = (int)(pl.sci_block.size() / 8);
     dp.sci_eP = pl.sci_eP, dp.sci_eAt = pl.sci_eAt, dp.sci_eA = pl.sci_eA;
-    dp.sci_Pi = pl.sci_Pi, dp.sci_Pc = pl.sci_Pc, dp.sci_Ai = pl.sci_Ai, dp.sci_Ac = pl.sci_Ac;
+    dp.sci_ra = pl.sci_ra, dp.sci_ca = pl.sci_ca;
 
     // occupancy (LDS image and VGPRs) -> persistent grid
     int dev = 0, ncu = 0;

@@ -1044,14 +1044,17 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     put(pl.ellP.src, pl.ellP.total, pl.sci_eP);
     put(pl.ellAt.src, pl.ellAt.total, pl.sci_eAt);
     put(pl.ellA.src, pl.ellA.total, pl.sci_eA);
-    put(pl.Pi, pl.nnzP, pl.sci_Pi);
-    put(pl.Pcol, pl.nnzP, pl.sci_Pc);
-    put(pl.Ai, pl.nnzA, pl.sci_Ai);
-    put(pl.Acol, pl.nnzA, pl.sci_Ac);
+    std::vector<uint16_t> ra, ca;
+    for (int k = 0; k < pl.nnzP; ++k)
+      ra.push_back((uint16_t)(pl.S_DT + pl.Pi[k])), ca.push_back((uint16_t)(pl.S_DT + pl.Pcol[k]));
+    for (int k = 0; k < pl.nnzA; ++k)
+      ra.push_back((uint16_t)(pl.S_ET + pl.Ai[k])), ca.push_back((uint16_t)(pl.S_DT + pl.Acol[k]));
+    put(ra, (int)ra.size(), pl.sci_ra);
+    put(ca, (int)ca.size(), pl.sci_ca);
     while (b.size() % 8) b.push_back(0);
     // ELL padding reads a zero double kept behind the value overlay (no conditional LDS reads)
     pl.S_ZERO = pl.S_ET + m;
-    for (int k = 0; k < pl.sci_Pi; ++k)
+    for (int k = 0; k < pl.sci_ra; ++k)
       if (b[k] == 0xffff) b[k] = (uint16_t)pl.S_ZERO;
     pl.SCI = ((pl.S_ZERO + 1) * 4 + 7) & ~7;  // u16 units, 16-byte aligned
     const int end = pl.SCI + (int)b.size();

@@ -116,7 +116,10 @@ struct Plan {
   // lists of P, A', A and the (row, column) of every P and A entry, copied in once per solve so
   // the Ruiz passes read indices from LDS; offsets relative to SCI
   int SCI = 0, S_ZERO = 0;  // S_ZERO: a zero double (in doubles) for the ELL padding
-  int sci_eP = 0, sci_eAt = 0, sci_eA = 0, sci_Pi = 0, sci_Pc = 0, sci_Ai = 0, sci_Ac = 0;
+  int sci_eP = 0, sci_eAt = 0, sci_eA = 0;
+  // the Ruiz rescale's operand slots of the value overlay [P | A] (CSC orders): row scaling slot
+  // (S_DT + i for P, S_ET + i for A) and column scaling slot (S_DT + j)
+  int sci_ra = 0, sci_ca = 0;
   std::vector<uint16_t> sci_block;  // padded to a multiple of 8 entries
   // KKT assembly: LDS slot of each P entry (diagonal -> D slot), A entry, rho diagonal,
   // sigma diagonal (D slot of x_j)

@@ -10,8 +10,8 @@ VARIANTS="${ABL_VARIANTS:-base SKIP_RHS SKIP_FWD SKIP_DIAG SKIP_BWD SKIP_UPDATE 
 if [ "$1" = build ]; then
   mkdir -p "$R/tools/abl"; C="$R/mpc_arpo_project_amd/csrc"
   for v in $VARIANTS; do
-    F="-DEXP_NOCHECK"; [ $v != base ] && for x in ${v//+/ }; do F="$F -DEXP_${x/@/=}"; done
-    [ $v = CHECK_NOEXIT ] && F="-DEXP_CHECK_NOEXIT"
+    F="-DEXP_NOCHECK"; [[ $v == *CHECK_NOEXIT* ]] && F=""
+    [ $v != base ] && for x in ${v//+/ }; do F="$F -DEXP_${x/@/=}"; done
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -DMPCQP_ONLY_SMALL $F \
       $C/engine.hip $C/closed_loop.hip $C/estimation.hip $C/symbolic.cpp $C/lds_layout.cpp $C/emulate.cpp \
       -o "$R/tools/abl/libmpcqp_$v.so" 2>&1 | grep -v hip-link &
