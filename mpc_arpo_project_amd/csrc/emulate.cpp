@@ -61,7 +61,7 @@ void run_fac_table(const std::vector<uint32_t>& tbl, int nsteps, std::vector<dou
   }
 }
 
-void run_solve_table(const std::vector<uint32_t>& tbl, int nsteps, std::vector<double>& v) {
+void run_solve_table(const std::vector<uint32_t>& tbl, int nsteps, bool paired, std::vector<double>& v) {
   double nq[4][64];
   for (int s = 0; s < nsteps; ++s) {
     const uint32_t* r = tbl.data() + (size_t)s * SOLVE_STEP_WORDS;
@@ -71,8 +71,13 @@ void run_solve_table(const std::vector<uint32_t>& tbl, int nsteps, std::vector<d
         const double x0 = v[w[0] / 8u], y0 = v[w[1] / 8u], x1 = v[w[2] / 8u], y1 = v[w[3] / 8u];
         nq[q][l] = std::fma(-x1, y1, -(x0 * y0));
       }
-    for (int q = 0; q < 4; ++q)  // the four ds_add_f64 instructions, in issue order
-      for (int l = 0; l < 64; ++l) v[r[SOLVE_TERM_WORDS + l * 4 + q] / 8u] += nq[q][l];
+    // the ds_add_f64 instructions in issue order: paired steps sum segments 0 + 1 in registers
+    // and add them to t0 (three atomics), unpaired steps add every segment to its own target
+    for (int q = 0; q < 4; ++q) {
+      if (paired && q == 1) continue;
+      for (int l = 0; l < 64; ++l)
+        v[r[SOLVE_TERM_WORDS + l * 4 + q] / 8u] += (paired && q == 0) ? nq[0][l] + nq[1][l] : nq[q][l];
+    }
   }
 }
 
@@ -96,16 +101,25 @@ bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, doubl
   for (int k = 0; k < pl.nnzL; ++k) v[pl.LX + k] *= v[pl.Lcol[k]];
   if (pl.ntail > 0) run_fac_table(pl.tail, pl.ntail, v);
   // one solve (the ADMM loop's vector passes around run_body(fwd) and run_body(bwd))
+  // right-hand side into C; W gets it on the copy rows and 0 elsewhere (every W slot is some
+  // lane's register-slot slot)
   const int coff = pl.CACC - pl.W;
-  for (int i = 0; i < 64 * pl.RN; ++i) v[pl.wsx[i] + coff] = i < n ? rhs[i] : 0.0;
-  for (int i = 0; i < 64 * pl.RM; ++i) v[pl.wsz[i] + coff] = i < m ? rhs[n + i] : 0.0;
-  for (int k = 0; k < pl.NKP; ++k) v[pl.W + k] = 0.0;
-  run_solve_table(pl.fwd, pl.nfwd, v);
+  for (int i = 0; i < 64 * pl.RN; ++i) {
+    const double b = i < n ? rhs[i] : 0.0;
+    v[pl.wsx[i] + coff] = b;
+    v[pl.wsx[i]] = (pl.wcopy[i % 64] >> (i / 64)) & 1u ? b : 0.0;
+  }
+  for (int i = 0; i < 64 * pl.RM; ++i) {
+    const double b = i < m ? rhs[n + i] : 0.0;
+    v[pl.wsz[i] + coff] = b;
+    v[pl.wsz[i]] = (pl.wcopy[i % 64] >> (pl.RN + i / 64)) & 1u ? b : 0.0;
+  }
+  run_solve_table(pl.fwd, pl.nfwd, pl.paired, v);
   for (int k = 0; k < pl.NKP; ++k) {
     v[pl.CACC + k] = v[pl.W + k] * v[pl.DINV + k];
     v[pl.W + k] = 0.0;
   }
-  run_solve_table(pl.bwd, pl.nbwd, v);
+  run_solve_table(pl.bwd, pl.nbwd, pl.paired, v);
   bool finite = true;
   for (int j = 0; j < n; ++j) sol[j] = v[pl.wsx[j]], finite = finite && std::isfinite(sol[j]);
   for (int i = 0; i < m; ++i) sol[n + i] = v[pl.wsz[i]], finite = finite && std::isfinite(sol[n + i]);

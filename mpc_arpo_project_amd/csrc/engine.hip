@@ -60,6 +60,7 @@ struct DevPlan {
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
   int NKS;  // 64-lane slots of the padded 1/D, W and C regions (symbolic.hpp NKP / 64 = RN + RM)
   // scaling index overlay (symbolic.hpp): 16-byte chunks copied to LDS at u16 offset SCI
+  const uint32_t* wcopy;  // per lane: register slots holding copy rows (symbolic.hpp Plan::wcopy)
   const uint4* sci_src;
   int SCI, S_ZERO, sci_n16, sci_eP, sci_eAt, sci_eA, sci_ra, sci_ca;
 };
@@ -189,7 +190,8 @@ __device__ __forceinline__ Rsrc table_rsrc(const uint32_t* tbl, int nsteps, int 
                                            nsteps * stride_words * 4, 0x00020000);
 }
 
-// one lane's records of a solve step: 4 segment quads (a0, b0, a1, b1), targets t0..t3
+// one lane's records of a solve step: 4 segment quads (a0, b0, a1, b1), targets t0..t3 (paired
+// steps: t1 = t0, not read)
 struct SolveRec {
   uint32_t a[SOLVE_MAXC], b[SOLVE_MAXC];
   uint32_t t0, t1, t2, t3;
@@ -250,6 +252,7 @@ __device__ __forceinline__ double dot3(const double* v, const FacRec& r) {
 __device__ __forceinline__ void lds_add(uint32_t a, double x) {
   __hip_atomic_fetch_add((lds_double*)(size_t)a, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+template <bool PAIRED>
 __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
   double x[8], y[8];
 #pragma unroll
@@ -267,8 +270,7 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
   const double n2 = fma(-x[5], y[5], -(x[4] * y[4]));
   const double n3 = fma(-x[7], y[7], -(x[6] * y[6]));
 #if defined(EXP_WRITE_NOT_ADD)  // timing ablation: plain stores instead of LDS atomics
-  lds_st(v, r.t0, n0);
-  lds_st(v, r.t1, n1);
+  lds_st(v, r.t0, n0 + n1);
   lds_st(v, r.t2, n2);
   lds_st(v, r.t3, n3);
 #elif defined(EXP_NO_ATOMIC)  // timing ablation: no LDS writes at all (keeps the values live)
@@ -276,16 +278,26 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
 #elif defined(EXP_MASKED_ADDS)  // timing ablation: atomics 1-3 issued with EXP_MASKED_ADDS lanes
   lds_add(r.t0, n0);
   if (__lane_id() < EXP_MASKED_ADDS) {
-    lds_add(r.t1, n1);
-    lds_add(r.t2, n2);
+    lds_add(r.t2, n1 + n2);
     lds_add(r.t3, n3);
   }
+#elif defined(EXP_SEQ01)  // diagnostic: the pair added as two atomics (the old rounding)
+  lds_add(r.t0, n0);
+  lds_add(r.t0, n1);
+  lds_add(r.t2, n2);
+  lds_add(r.t3, n3);
 #elif defined(EXP_TWO_ADDS)  // timing ablation: two atomics per lane
   lds_add(r.t0, n0 + n1);
   lds_add(r.t2, n2 + n3);
 #else
-  lds_add(r.t0, n0);
-  lds_add(r.t1, n1);
+  if constexpr (PAIRED) {
+    // segments 0 and 1 are a pair of one target (or segment 1 is unused: its zero-padding terms
+    // give -0, and n0 + -0 == n0 exactly) -- one atomic for both
+    lds_add(r.t0, n0 + n1);
+  } else {
+    lds_add(r.t0, n0);
+    lds_add(r.t1, n1);
+  }
   lds_add(r.t2, n2);
   lds_add(r.t3, n3);
 #endif
@@ -360,6 +372,7 @@ __device__ __forceinline__ void run_body(Rsrc rs, int n, uint32_t lane, const Op
   }
 }
 #undef MPCQP_STEP
+template <bool PAIRED>
 struct SolveOps {
   typedef SolveRec Rec;
   static constexpr int STRIDE = SOLVE_STEP_WORDS;
@@ -367,7 +380,7 @@ struct SolveOps {
   __device__ __forceinline__ static void load(Rsrc rs, int soff, uint32_t lane, Rec& r) {
     load_solve(rs, soff, lane, r);
   }
-  __device__ __forceinline__ void step(const Rec& r, int) const { solve_step(r, v); }
+  __device__ __forceinline__ void step(const Rec& r, int) const { solve_step<PAIRED>(r, v); }
 };
 struct FacOps {
   typedef FacRec Rec;
@@ -1056,7 +1069,7 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
   LDS_FENCE();
 }
 
-template <int RN, int RM>
+template <int RN, int RM, bool PAIRED>
 __device__ __forceinline__ void solve_instance(const KParams& p, int inst, double* v, double* scr,
                                                int lane) {
   const DevPlan& P = p.pl;
@@ -1136,6 +1149,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #pragma unroll
   for (int r = 0; r < RM; ++r) wsz[r] = (int)P.wsz[lane + 64 * r];
   const int coff = P.CACC - P.W;  // rhs goes to the accumulator region, the solution comes back in W
+  const uint32_t wcp = P.wcopy[lane];
   // loop constants held in VGPRs (an opaque copy: otherwise they are re-read from the kernel
   // arguments inside the loop, with an lgkmcnt(0) wait that also drains the LDS queue)
   double sigma = p.s.sigma, alpha = p.s.alpha, alpha_c = 1.0 - p.s.alpha;
@@ -1149,8 +1163,8 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   bool can_check = false;
   double dx[RN], dy[RM];
   Resid<RN, RM> R;
-  Pipe<SolveOps> sp;
-  const SolveOps sops{v};
+  Pipe<SolveOps<PAIRED>> sp;
+  const SolveOps<PAIRED> sops{v};
   const Rsrc rs_fwd = table_rsrc(P.fwd, P.nfwd, SOLVE_STEP_WORDS);
   const Rsrc rs_bwd = table_rsrc(P.bwd, P.nbwd, SOLVE_STEP_WORDS);
   for (iter = 1; iter <= p.s.max_iter; ++iter) {
@@ -1161,20 +1175,22 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
     // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
 #ifndef EXP_SKIP_RHS  // timing ablations (tools/ablate_fixed.sh): EXP_NOCHECK + EXP_SKIP_*
+    // The forward solve accumulates into W, which starts at 0 except on the copy rows (first
+    // block, empty reach: W_r = rhs_r, no solve task); the lanes' slots cover all of W
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       xp[r] = S.x[r];
-      v[wsx[r] + coff] = sigma * xp[r] - S.q[r];
+      const double b = sigma * xp[r] - S.q[r];
+      v[wsx[r] + coff] = b;
+      v[wsx[r]] = (wcp >> r) & 1u ? b : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       zp[r] = S.z[r];
       bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
       v[wsz[r] + coff] = bz[r];
+      v[wsz[r]] = (wcp >> (RN + r)) & 1u ? bz[r] : 0.0;
     }
-#pragma unroll
-    for (int r = 0; r < RN + RM; ++r)  // the solve accumulates into W (NKP = 64 (RN + RM))
-      v[P.W + lane + 64 * r] = 0.0;
 #else
 #pragma unroll
     for (int r = 0; r < RN; ++r) xp[r] = S.x[r];
@@ -1376,7 +1392,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #ifndef MPCQP_WAVES_PER_EU
 #define MPCQP_WAVES_PER_EU 1
 #endif
-template <int RN, int RM>
+template <int RN, int RM, bool PAIRED>
 __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = (int)threadIdx.x;
@@ -1390,7 +1406,7 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
     inst = __builtin_amdgcn_readfirstlane(inst);
     if (inst >= (unsigned int)p.B) break;
     if (p.skip && p.skip[inst]) continue;  // wave-uniform
-    solve_instance<RN, RM>(p, (int)inst, v, scr, lane);
+    solve_instance<RN, RM, PAIRED>(p, (int)inst, v, scr, lane);
     LDS_FENCE();
   }
 }
@@ -1418,18 +1434,18 @@ int cap_m() { return env_int("MPCQP_CAPM", 0); }  // 0: chosen per structure
 int cap_w() { return env_int("MPCQP_CAPW", 0); }
 
 template <int RN, int RM>
-kernel_fn pick() {
-  return qp_batch_kernel<RN, RM>;
+kernel_fn pick(bool paired) {
+  return paired ? qp_batch_kernel<RN, RM, true> : qp_batch_kernel<RN, RM, false>;
 }
 
-// RN = ceil(n/64) and RM = ceil(m/64) rounded up to the instantiated buckets
-kernel_fn select_kernel(int n, int m) {
+// RN = ceil(n/64) and RM = ceil(m/64) rounded up to the instantiated buckets; the plan's step kind
+kernel_fn select_kernel(int n, int m, bool paired) {
   int rn = 0, rm = 0;
   if (!kernel_bucket(n, m, rn, rm)) return nullptr;
-  if (rn == 2) return pick<2, 4>();
+  if (rn == 2) return pick<2, 4>(paired);
 #ifndef MPCQP_ONLY_SMALL
-  if (rn == 4) return pick<4, 8>();
-  if (rn == 8) return pick<8, 16>();
+  if (rn == 4) return pick<4, 8>(paired);
+  if (rn == 8) return pick<8, 16>(paired);
 #endif
   return nullptr;
 }
@@ -1538,7 +1554,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     return fail(code, msg);
   };
   {
-    h->kern = select_kernel(pl.n, pl.m);
+    h->kern = select_kernel(pl.n, pl.m, pl.paired);
     if (!h->kern) {
       delete h;
       return fail(MPCQP_E_UNSUPPORTED, "problem dimensions exceed the instantiated kernels");
@@ -1559,7 +1575,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
            o_eAi = push_blob(blob, pl.ellA.in), o_eTs = push_blob(blob, pl.ellAt.src),
            o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
            o_ePi = push_blob(blob, pl.ellP.in), o_sci = push_blob(blob, pl.sci_block),
-           o_pA = push_blob(blob, pl.posA), o_pP = push_blob(blob, pl.posP);
+           o_pA = push_blob(blob, pl.posA), o_pP = push_blob(blob, pl.posP),
+           o_wc = push_blob(blob, pl.wcopy);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
@@ -1574,6 +1591,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.posA = (const uint16_t*)(b + o_pA), dp.posP = (const uint16_t*)(b + o_pP);
     dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
     dp.wsx = (const uint16_t*)(b + o_wx), dp.wsz = (const uint16_t*)(b + o_wz);
+    dp.wcopy = (const uint32_t*)(b + o_wc);
     dp.Ap = (const uint16_t*)(b + o_Ap), dp.Ai = (const uint16_t*)(b + o_Ai);
     dp.Acol = (const uint16_t*)(b + o_Ac), dp.Arp = (const uint16_t*)(b + o_Arp);
     dp.Ark = (const uint16_t*)(b + o_Ark), dp.Arj = (const uint16_t*)(b + o_Arj);

@@ -150,6 +150,7 @@ struct Opt {
     return read_cost_s(a, cnt, nz);
   }
   int at_group(const Step& s, int q, int grp) const {
+    if (q == 1 && pl.paired) return 0;  // segment 1 is summed into segment 0's atomic
     int a[16], cnt = 0;
     for (int l = 16 * grp; l < 16 * grp + 16; ++l) {
       const int t = s[q * 64 + l].t;
@@ -174,9 +175,9 @@ struct Opt {
         int a[64];
         for (int l = 0; l < 64; ++l) a[l] = ws[64 * r + l] - pl.W;  // vector index
         for (int g = 0; g < 4; ++g) {
-          int p[16];
-          for (int l = 0; l < 16; ++l) p[l] = ren[pl.CACC + a[16 * g + l]];
-          c += write_cost_s(p, 16);
+          int p[16], w[16];
+          for (int l = 0; l < 16; ++l) p[l] = ren[pl.CACC + a[16 * g + l]], w[l] = ren[pl.W + a[16 * g + l]];
+          c += write_cost_s(p, 16) + write_cost_s(w, 16);
         }
         for (int h = 0; h < 2; ++h) {
           int p[32];
@@ -218,17 +219,44 @@ struct Opt {
       for (auto& g : groups) c += g[0] == 0 ? rd_group(s, g[1] / 2, g[1] % 2, g[2]) : at_group(s, g[1], g[2]);
       return c;
     };
+    // pair rule: segment 1 of a lane is unused or belongs to segment 0's target
+    auto lane_ok = [&](int l) {
+      return !pl.paired || s[64 + l].t < 0 || (s[l].t >= 0 && s[l].t == s[64 + l].t);
+    };
     Step best = s;
     int bestc = cur;
     for (int it = 0; it < moves; ++it) {
       if (cur < bestc) bestc = cur, best = s;
       const double T = T0 * std::pow(T1 / T0, (double)it / moves);
-      const int kind = rng.below(8);
+      const int kind = rng.below(9);
       groups.clear();
-      if (kind < 4) {  // swap two positions (at least one used)
+      if (kind == 8) {  // swap the pairs (segments 0 and 1) of two lanes
+        const int l1 = rng.below(64), l2 = rng.below(64);
+        if (l1 == l2 || (s[l1].t < 0 && s[l2].t < 0)) continue;
+        for (int q = 0; q < 2; ++q) add_pos(q * 64 + l1), add_pos(q * 64 + l2);
+        const int before = gcost();
+        std::swap(s[l1], s[l2]), std::swap(s[64 + l1], s[64 + l2]);
+        const int d = gcost() - before;
+        if (d <= 0 || rng.unit() < std::exp(-d / T)) {
+          cur += d;
+          for (int& u : used)
+            for (int q = 0; q < 2; ++q) {
+              if (u == q * 64 + l1)
+                u = q * 64 + l2;
+              else if (u == q * 64 + l2)
+                u = q * 64 + l1;
+            }
+        } else {
+          std::swap(s[l1], s[l2]), std::swap(s[64 + l1], s[64 + l2]);
+        }
+      } else if (kind < 4) {  // swap two positions (at least one used)
         const int p1 = used[rng.below((int)used.size())];
         int p2 = rng.below(256);
         if (p2 == p1) continue;
+        std::swap(s[p1], s[p2]);
+        const bool ok = lane_ok(p1 % 64) && lane_ok(p2 % 64);
+        std::swap(s[p1], s[p2]);
+        if (!ok) continue;
         add_pos(p1), add_pos(p2);
         const int before = gcost();
         std::swap(s[p1], s[p2]);
@@ -278,8 +306,11 @@ struct Opt {
     if (cur < bestc) bestc = cur, best = s;
     s = best;
     // a segment whose two terms both became padding adds nothing: unused (its target frees a bank)
-    for (Seg& g : s)
-      if (g.t >= 0 && g.a[0] < 0 && g.a[1] < 0) g.t = -1;
+    // -- unless it is segment 0 of a pair whose segment 1 is used (that sum needs the atomic)
+    for (int p = 0; p < 256; ++p) {
+      Seg& g = s[p];
+      if (g.t >= 0 && g.a[0] < 0 && g.a[1] < 0 && !(pl.paired && p < 64 && s[64 + p].t >= 0)) g.t = -1;
+    }
   }
 
   // ---- phase B: slot permutations (positions fixed)
@@ -314,20 +345,26 @@ struct Opt {
             }
             G.push_back(std::move(g));
           }
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q) {
+        if (q == 1 && pl.paired) continue;  // summed into segment 0's atomic
         for (int grp = 0; grp < 4; ++grp) {
           Group g{1, 0, {}, 0};
           for (int l = 16 * grp; l < 16 * grp + 16; ++l)
             if (s[q * 64 + l].t >= 0) g.mem.push_back(s[q * 64 + l].t);
           G.push_back(std::move(g));
         }
+      }
     }
     auto pass = [&](const std::vector<uint16_t>& ws, int slots) {
       for (int r = 0; r < slots; ++r) {
         for (int grp = 0; grp < 4; ++grp) {
-          Group g{1, 0, {}, 0};
-          for (int l = 16 * grp; l < 16 * grp + 16; ++l) g.mem.push_back(pl.CACC + ws[64 * r + l] - pl.W);
+          Group g{1, 0, {}, 0}, gw{1, 0, {}, 0};
+          for (int l = 16 * grp; l < 16 * grp + 16; ++l) {
+            g.mem.push_back(pl.CACC + ws[64 * r + l] - pl.W);
+            gw.mem.push_back(ws[64 * r + l]);
+          }
           G.push_back(std::move(g));
+          G.push_back(std::move(gw));
         }
         for (int h = 0; h < 2; ++h) {
           Group g{0, 0, {}, 0};
@@ -470,6 +507,7 @@ struct Opt {
             }
         for (int q = 0; q < 4; ++q)
           for (int grp = 0; grp < 4; ++grp) {
+            if (q == 1 && pl.paired) continue;  // segment 1 of a pair: no atomic (its word repeats t0 below)
             int c[WBANKS] = {};
             for (int l = 16 * grp; l < 16 * grp + 16; ++l)
               if (S[q * 64 + l].t >= 0) c[ren[S[q * 64 + l].t] & (WBANKS - 1)]++;
@@ -487,6 +525,8 @@ struct Opt {
               r[SOLVE_TERM_WORDS + l * 4 + q] = slot * 8u;
             }
           }
+        if (pl.paired)
+          for (int l = 0; l < 64; ++l) r[SOLVE_TERM_WORDS + l * 4 + 1] = r[SOLVE_TERM_WORDS + l * 4 + 0];
       }
     }
     // every other table: relabel slots
@@ -529,26 +569,27 @@ LdsModel model_lds(const Plan& pl) {
           }
       for (int q = 0; q < 4; ++q)
         for (int g = 0; g < 4; ++g) {
+          if (q == 1 && pl.paired) continue;  // segments 0 + 1 share one atomic
           int a[16];
           for (int l = 0; l < 16; ++l) a[l] = (int)(r[SOLVE_TERM_WORDS + (16 * g + l) * 4 + q] / 8u);
           m.atomic += write_cost(a, 16);
         }
-      m.floor += 32 + 16;
+      m.floor += 32 + (pl.paired ? 12 : 16);
     }
   }
   auto pass = [&](const std::vector<uint16_t>& ws, int slots) {
     for (int r = 0; r < slots; ++r) {
       for (int g = 0; g < 4; ++g) {
-        int a[16];
-        for (int l = 0; l < 16; ++l) a[l] = pl.CACC - pl.W + ws[64 * r + 16 * g + l];
-        m.vec += write_cost(a, 16);
+        int a[16], w[16];
+        for (int l = 0; l < 16; ++l) a[l] = pl.CACC - pl.W + ws[64 * r + 16 * g + l], w[l] = ws[64 * r + 16 * g + l];
+        m.vec += write_cost(a, 16) + write_cost(w, 16);
       }
       for (int h = 0; h < 2; ++h) {
         int a[32];
         for (int l = 0; l < 32; ++l) a[l] = ws[64 * r + 32 * h + l];
         m.vec += read_cost(a, 32, 0);
       }
-      m.floor += 6;
+      m.floor += 10;
     }
   };
   pass(pl.wsx, pl.RN);

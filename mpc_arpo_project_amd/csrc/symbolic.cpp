@@ -155,12 +155,8 @@ int pack_fac_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<u
 // addresses serialise): each segment goes to the free (lane, segment) position whose vector
 // operands and target collide least with those already placed.  The matrix operands are made
 // conflict-free afterwards by permuting their LDS slots (layout_matrix_values).
-int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<uint32_t>& tbl) {
-  if (getenv("MPCQP_DUMP_TASKS")) {
-    fprintf(stderr, "level:");
-    for (const Task& t : tasks) fprintf(stderr, " %zu", t.terms.size());
-    fprintf(stderr, "\n");
-  }
+// unpaired steps: four independent segments per lane, four atomics
+int pack_solve_level_free(const std::vector<Task>& tasks, const Plan& pl, std::vector<uint32_t>& tbl) {
   struct Seg {
     int target;
     int a0, b0, a1, b1;
@@ -222,6 +218,142 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
     }
     nsteps++;
     s0 = s1;
+  }
+  return nsteps;
+}
+
+int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<uint32_t>& tbl) {
+  if (getenv("MPCQP_DUMP_TASKS")) {
+    fprintf(stderr, "level:");
+    for (const Task& t : tasks) fprintf(stderr, " %c%zu", t.target >= pl.W && t.target < pl.W + pl.NKP ? 'w' : 'c', t.terms.size());
+    fprintf(stderr, "\n");
+  }
+  if (!pl.paired) return pack_solve_level_free(tasks, pl, tbl);
+  struct Seg {
+    int target;
+    int a0, b0, a1, b1;
+  };
+  // remaining segments per target, in task order
+  std::vector<std::vector<Seg>> rem;
+  for (const Task& t : tasks) {
+    std::vector<Seg> v;
+    for (size_t k = 0; k < t.terms.size(); k += 2) {
+      Seg g{t.target, t.terms[k][0], t.terms[k][1], pl.ZERO, pl.ZERO};
+      if (k + 1 < t.terms.size()) g.a1 = t.terms[k + 1][0], g.b1 = t.terms[k + 1][1];
+      v.push_back(g);
+    }
+    if (!v.empty()) rem.push_back(std::move(v));
+  }
+  const uint32_t zb = (uint32_t)pl.ZERO * 8u;
+  int nsteps = 0;
+  auto left = [&]() {
+    for (auto& v : rem)
+      if (!v.empty()) return true;
+    return false;
+  };
+  while (left()) {
+    const size_t base = tbl.size();
+    tbl.resize(base + SOLVE_STEP_WORDS, zb);
+    uint32_t* terms = tbl.data() + base;
+    uint32_t* tg = terms + SOLVE_TERM_WORDS;
+    for (int l = 0; l < 64; ++l)
+      for (int q = 0; q < 4; ++q) tg[l * 4 + q] = (uint32_t)(pl.SINK + l) * 8u;
+    // this step's units: pairs (two segments of one target, lane positions 0 + 1) first, most
+    // segments first; then single segments into positions 2 / 3, then into free pair positions
+    std::vector<std::vector<Seg>> units;
+    {
+      std::vector<int> ord(rem.size());
+      for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+      std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return rem[x].size() > rem[y].size(); });
+      int pairs = 64, singles = 128;
+      for (int i : ord)
+        while (rem[i].size() >= 2 && pairs > 0) {
+          units.push_back({rem[i][0], rem[i][1]});
+          rem[i].erase(rem[i].begin(), rem[i].begin() + 2);
+          pairs--;
+        }
+      for (int i : ord)
+        while (!rem[i].empty() && (singles > 0 || pairs > 0)) {
+          units.push_back({rem[i][0]});
+          rem[i].erase(rem[i].begin());
+          if (singles > 0)
+            singles--;
+          else
+            pairs--;
+        }
+    }
+    // placement: the free position whose operands and target collide least with those placed
+    // (ds_read_b64: two 32-lane halves, bank = slot mod 32, broadcast; ds_add_f64: four 16-lane
+    // groups, bank = slot mod 16) -- the layout optimiser refines it
+    std::vector<std::vector<int>> rd(8 * 2 * 32);
+    std::vector<int> at(4 * 4 * 16, 0);
+    std::vector<char> used(256, 0);  // position q * 64 + lane
+    auto rd_pen = [&](int c, int h, int b) {
+      if (b == pl.ZERO) return 0;
+      const auto& v = rd[(c * 2 + h) * 32 + b % 32];
+      for (int x : v)
+        if (x == b) return 0;  // broadcast
+      return (int)v.size();
+    };
+    auto add_rd = [&](int c, int h, int b) {
+      if (b == pl.ZERO) return;
+      auto& v = rd[(c * 2 + h) * 32 + b % 32];
+      if (std::find(v.begin(), v.end(), b) == v.end()) v.push_back(b);
+    };
+    auto put = [&](int q, int l, const Seg& g) {
+      const int h = l / 32;
+      used[q * 64 + l] = 1;
+      add_rd(2 * q, h, g.b0);
+      add_rd(2 * q + 1, h, g.b1);
+      uint32_t* w = terms + q * 256 + l * 4;  // segment row q, lane quad (a0, b0, a1, b1)
+      w[0] = (uint32_t)g.a0 * 8u, w[1] = (uint32_t)g.b0 * 8u;
+      w[2] = (uint32_t)g.a1 * 8u, w[3] = (uint32_t)g.b1 * 8u;
+      tg[l * 4 + q] = (uint32_t)g.target * 8u;
+    };
+    int npairs = 0;
+    for (const auto& u : units) npairs += u.size() == 2;
+    int placed_pairs = 0;
+    for (const auto& u : units) {
+      const Seg& g = u[0];
+      int best = -1, bestp = 1 << 30;
+      if (u.size() == 2) {
+        for (int l = 0; l < 64; ++l) {
+          if (used[l]) continue;
+          const int h = l / 32;
+          int pen = 4 * at[(0 * 4 + l / 16) * 16 + g.target % 16];
+          pen += rd_pen(0, h, g.b0) + rd_pen(1, h, g.b1) + rd_pen(2, h, u[1].b0) + rd_pen(3, h, u[1].b1);
+          if (pen < bestp) bestp = pen, best = l;
+          if (pen == 0) break;
+        }
+        put(0, best, g);
+        put(1, best, u[1]);
+        at[(0 * 4 + best / 16) * 16 + g.target % 16]++;
+        placed_pairs++;
+        continue;
+      }
+      // a single: positions 2 / 3 first; a free pair position (segment 0, segment 1 unused) only
+      // when those are full, and never one a later pair needs
+      int free_pairs = 0;
+      for (int l = 0; l < 64; ++l) free_pairs += !used[l];
+      const bool pair_ok = free_pairs > npairs - placed_pairs;
+      for (int pass = 0; pass < 2 && best < 0; ++pass)
+        for (int pos = 0; pos < 256; ++pos) {
+          const int q = pos / 64, l = pos % 64;
+          if (used[pos] || q == 1 || (pass == 0) != (q >= 2) || (q == 0 && !pair_ok)) continue;
+          const int h = l / 32;
+          int pen = 4 * at[(q * 4 + l / 16) * 16 + g.target % 16];
+          pen += rd_pen(2 * q, h, g.b0) + rd_pen(2 * q + 1, h, g.b1);
+          if (pen < bestp) bestp = pen, best = pos;
+          if (pen == 0) break;
+        }
+      const int q = best / 64, l = best % 64;
+      put(q, l, g);
+      if (q == 0) used[64 + l] = 1;  // segment 1 of this lane stays unused
+      at[(q * 4 + l / 16) * 16 + g.target % 16]++;
+    }
+    // segment 1 of a pair repeats t0 (not read by the kernel; keeps the tables self-describing)
+    for (int l = 0; l < 64; ++l) tg[l * 4 + 1] = tg[l * 4 + 0];
+    nsteps++;
   }
   return nsteps;
 }
@@ -519,8 +651,9 @@ std::vector<std::vector<Task>> place_accumulations(std::vector<std::vector<Task>
 }
 
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, Plan& pl, int capM, int capW) {
+                const int32_t* Ai, Plan& pl, int capM, int capW, bool paired) {
   pl = Plan();
+  pl.paired = paired;
   pl.n = n, pl.m = m, pl.nk = n + m;
   const int nk = n + m;
   pl.nnzP = Pp[n];
@@ -796,6 +929,16 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     pl.wsx[i] = (uint16_t)(pl.W + (i < n ? pl.pinv[i] : nk + (i - n)));
   for (int i = 0; i < 64 * pl.RM; i++)
     pl.wsz[i] = (uint16_t)(pl.W + (i < m ? pl.pinv[n + i] : nk + (64 * pl.RN - n) + (i - m)));
+  pl.wcopy.assign(64, 0u);
+  {
+    auto is_copy = [&](int row) { return blk[row] == 0 && reach[row].empty(); };
+    for (int l = 0; l < 64; ++l) {
+      for (int r = 0; r < pl.RN; ++r)
+        if (l + 64 * r < n && is_copy(pl.pinv[l + 64 * r])) pl.wcopy[l] |= 1u << r;
+      for (int r = 0; r < pl.RM; ++r)
+        if (l + 64 * r < m && is_copy(pl.pinv[n + l + 64 * r])) pl.wcopy[l] |= 1u << (pl.RN + r);
+    }
+  }
 
   // ---- levels
   std::vector<int> lev(nk, 0), blev(nk, 0);
@@ -920,6 +1063,9 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     std::vector<AccTerm> acc;
     for (int k = 0; k < T; k++)
       for (int r = bs(k); r < be(k); r++) {
+        // a row of the first block with an empty reach is a copy: W_r = C_r = rhs_r, stored by
+        // the right-hand side pass (Plan::wcopy), no solve task
+        if (k == 0 && reach[r].empty()) continue;
         Task t;
         t.target = pl.W + r;
         for (int r2 : reach[r]) t.terms.push_back({nslot(r, r2), pl.CACC + r2, 0});
@@ -1076,8 +1222,9 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
                       int max_per_cu) {
   // the LDS layout optimiser runs on the chosen plan (MPCQP_NO_ANNEAL=1: off, diagnostics)
   const bool anneal = !getenv("MPCQP_NO_ANNEAL") && !getenv("MPCQP_NO_LAYOUT");
+  const char* fp = getenv("MPCQP_PAIRED");  // diagnostics: force the step kind
   if (capM > 0 && capW > 0) {
-    if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW)) return false;
+    if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW, !fp || atoi(fp) != 0)) return false;
     if (anneal) optimize_lds(plan);
     return true;
   }
@@ -1086,6 +1233,7 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
   std::vector<int32_t> key;
   key.push_back(n), key.push_back(m), key.push_back(lds_per_cu), key.push_back(max_per_cu);
   key.push_back(anneal);
+  key.push_back(fp ? atoi(fp) : -1);
   key.insert(key.end(), Pp, Pp + n + 1);
   key.insert(key.end(), Pi, Pi + Pp[n]);
   key.insert(key.end(), Ap, Ap + n + 1);
@@ -1100,26 +1248,37 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
       return true;
     }
   }
-  static const int CM[] = {96, 112, 128, 144, 160, 176, 192, 224, 256};
+  // Block caps stop at 192 and, among equally fast plans, the smallest blocks win: a block
+  // inverse's entries grow with the block, and so does the rounding of the blocked substitution on
+  // ill-conditioned (warm, large-rho) KKT systems -- at N = 20 a 192-row cap plan has the 176-row
+  // plan's 13 steps but cuts the warm lockstep status agreement with the oracle from 0.995 to 0.96
+  // (tests/test_gpu_scale_parity.py); larger caps are not validated against the oracle
+  static const int CM[] = {96, 112, 128, 144, 160, 176, 192};
   static const int CW[] = {320, 352, 384, 416, 448, 480};
   bool found = false;
-  int best[4] = {0, 0, 0, 0};  // -per_cu, solve steps, fac steps, lds bytes
+  int best[5] = {0, 0, 0, 0, 0};  // -per_cu, step cost, block cap, fac steps, lds bytes
   int bm = 128, bw = 384;
-  for (int cm : CM)
-    for (int cw : CW) {
-      Plan pl;
-      if (!build_plan(n, m, Pp, Pi, Ap, Ai, pl, cm, cw)) continue;
-      const int lds = ((pl.LDS_N + 1) & ~1) * 8;
-      const int per_cu = std::min(max_per_cu, lds_per_cu / std::max(lds, 1));
-      const int sc[4] = {-per_cu, pl.nfwd + pl.nbwd, pl.nfac + pl.ntail, lds};
-      if (!found || std::lexicographical_compare(sc, sc + 4, best, best + 4)) {
-        found = true;
-        std::copy(sc, sc + 4, best);
-        bm = cm, bw = cw;
+  bool bp = true;
+  for (int pk = 1; pk >= 0; --pk) {
+    if (fp && atoi(fp) != pk) continue;
+    for (int cm : CM)
+      for (int cw : CW) {
+        Plan pl;
+        if (!build_plan(n, m, Pp, Pi, Ap, Ai, pl, cm, cw, pk != 0)) continue;
+        const int lds = ((pl.LDS_N + 1) & ~1) * 8;
+        const int per_cu = std::min(max_per_cu, lds_per_cu / std::max(lds, 1));
+        const int cost = (pl.nfwd + pl.nbwd) * (pk ? 92 : 100);
+        const int sc[5] = {-per_cu, cost, cm, pl.nfac + pl.ntail, lds};
+        if (!found || std::lexicographical_compare(sc, sc + 5, best, best + 5)) {
+          found = true;
+          std::copy(sc, sc + 5, best);
+          bm = cm, bw = cw, bp = pk != 0;
+        }
       }
-    }
+  }
   if (!found) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);  // reports the error
-  if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw)) return false;
+  if (getenv("MPCQP_DUMP_CAPS")) fprintf(stderr, "caps %d %d paired %d\n", bm, bw, (int)bp);
+  if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw, bp)) return false;
   if (anneal) optimize_lds(plan);
   {
     std::lock_guard<std::mutex> g(mu);

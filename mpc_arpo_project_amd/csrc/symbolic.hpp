@@ -34,7 +34,9 @@ constexpr int FAC_MAXC = 4;     // terms per lane of a factorization step
 // factorization step: meta[64] | FAC_MAXC rows of 64 (a, b, c, 0) quads
 constexpr int FAC_STEP_WORDS = 64 + 64 * 4 * FAC_MAXC;
 // solve step: SOLVE_MAXC / 2 rows of 64 segment quads (a0, b0, a1, b1) | 64 target quads
-// (t0, t1, t2, t3); segment q of a lane is added to its target t_q with an LDS atomic
+// (t0, t1, t2, t3); segments 0 and 1 of a lane are a PAIR: they belong to the same target (or
+// segment 1 is unused) and their sum is added to t0 with one LDS atomic; segments 2 and 3 are added
+// to t2 and t3 -- three atomics per lane and step (t1 repeats t0 and is not read)
 constexpr int SOLVE_TERM_WORDS = 64 * 2 * SOLVE_MAXC;
 constexpr int SOLVE_STEP_WORDS = SOLVE_TERM_WORDS + 64 * 4;
 
@@ -127,6 +129,11 @@ struct Plan {
   // LDS slot (permuted position in the W region) of x_i and z_i for every lane of the kernel's
   // register slots (64 RN and 64 RM entries; padding lanes get the W padding slots)
   std::vector<uint16_t> wsx, wsz;
+  // per lane, bit r: register slot r (x slots 0..RN-1, then z slots) holds a COPY row -- a row of
+  // the first block with an empty reach, whose forward-solve output is its right-hand side
+  // (W_r = C_r): the right-hand side pass stores it into W directly and no solve task computes it
+  std::vector<uint32_t> wcopy;
+  bool paired = true;  // solve-step kind (build_plan)
   // schedules (STEP_WORDS words per step): factorization of U = L D and D by levels, then
   // (after the flat pass L = U * (1/D)_col) the block-inverse tail; forward and backward solves
   std::vector<uint32_t> fac, tail, fwd, bwd;
@@ -149,13 +156,17 @@ struct Plan {
 
 // Builds the plan; returns false (with plan.error set) if the structure is unsupported.
 // capM / capW: per block, max entries of the block inverse and max solve terms of its w-tasks.
+// paired: solve steps with segments 0 + 1 of a lane on one target (three atomics per lane and
+// step, SOLVE_TERM_WORDS above) or with four independent segments (four atomics).
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, Plan& plan, int capM = 128, int capW = 384);
+                const int32_t* Ai, Plan& plan, int capM = 128, int capW = 384, bool paired = true);
 
-// build_plan with the block caps chosen per structure: over a grid of (capM, capW), the plan with
-// the most instances per CU (LDS image within lds_per_cu / k for k <= max_per_cu), then the fewest
-// solve steps per ADMM iteration, then the fewest factorization steps.  capM / capW > 0 force a
-// single build.  Results are memoised per structure within the process.
+// build_plan with the block caps and the step kind chosen per structure: over a grid of (capM <=
+// 192, capW) x {paired, unpaired}, the plan with the most instances per CU (LDS image within
+// lds_per_cu / k for k <= max_per_cu), then the least solve-step cost per ADMM iteration (a paired
+// step costs 0.92 of an unpaired one: one atomic of four saved), then the smallest blocks, then the
+// fewest factorization steps.  capM / capW > 0 force a single build (MPCQP_PAIRED=0/1 forces the
+// step kind).  Results are memoised per structure within the process.
 bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                       const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu = 163840,
                       int max_per_cu = 4);

@@ -55,5 +55,5 @@ def test_layout_optimiser_lowers_modelled_lds_cycles(monkeypatch):
     monkeypatch.setenv("MPCQP_NO_ANNEAL", "1")
     _, greedy = _lib.schedule_check(*args)
     tot = lambda d: d["read"] + d["atomic"] + d["vec"]
-    assert opt["floor"] == greedy["floor"] == 13 * 48 + 6 * 6
+    assert opt["floor"] == greedy["floor"] == 13 * 44 + 6 * 10
     assert tot(opt) < 0.8 * tot(greedy), (opt, greedy)
