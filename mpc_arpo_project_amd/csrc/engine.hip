@@ -88,7 +88,7 @@ struct KParams {
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
 // s_memtime deltas accumulated per wave in SGPRs, added to p.timing at the end of each instance.
-enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_V0, T_V1, T_V2, T_RS0, T_RS1, T_RS2, T_RS3, T_RS4, T_NSLOT };
+enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_V0, T_V1, T_V2, T_RS0, T_RS1, T_RS2, T_RS3, T_RS4, T_TM0, T_TM1, T_TM2, T_NSLOT };
 #ifdef MPCQP_TIMING
 #define T_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define T_END(slot, v) tacc[slot] += __builtin_amdgcn_s_memtime() - (v)
@@ -829,7 +829,8 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
 template <int RN, int RM>
 __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>& S, const Resid<RN, RM>& R,
                                  double (&dy)[RM], const double (&dx)[RN], const Slab& sb,
-                                 double* v, int lane, bool approximate) {
+                                 double* v, int lane, bool approximate TACC_PARAM) {
+  T_BEGIN(t_m0);
   const DevPlan& P = p.pl;
   double eps_abs = p.s.eps_abs, eps_rel = p.s.eps_rel;
   double eps_pinf = p.s.eps_prim_inf, eps_dinf = p.s.eps_dual_inf;
@@ -860,14 +861,20 @@ __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>&
   const double eps_prim = eps_abs + eps_rel * dmaxd(zn, axn);
   const double eps_dual = eps_abs + eps_rel * (dmaxd(dmaxd(qn, atn), pxn) * S.cinv);
   bool prim_ok = false, dual_ok = false, prim_inf = false, dual_inf = false;
+  TSYNC(eps_dual);
+  T_END(T_TM0, t_m0);
+  T_BEGIN(t_m1);
   if (S.pri_res < eps_prim)
     prim_ok = true;
   else
     prim_inf = is_primal_infeasible(p, S, dy, sb, v, lane, eps_pinf);
+  T_END(T_TM1, t_m1);
+  T_BEGIN(t_m2);
   if (S.dua_res < eps_dual)
     dual_ok = true;
   else
     dual_inf = is_dual_infeasible(p, S, dx, sb, v, lane, eps_dinf);
+  T_END(T_TM2, t_m2);
   if (prim_ok && dual_ok) return approximate ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED;
   if (prim_inf) return approximate ? MPCQP_PRIMAL_INFEASIBLE_INACCURATE : MPCQP_PRIMAL_INFEASIBLE;
   if (dual_inf) return approximate ? MPCQP_DUAL_INFEASIBLE_INACCURATE : MPCQP_DUAL_INFEASIBLE;
@@ -1278,7 +1285,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       continue;
 #endif
       T_BEGIN(t_tm);
-      status = check_termination(p, S, R, dy, dx, sb, v, lane, false);
+      status = check_termination(p, S, R, dy, dx, sb, v, lane, false TACC_ARG);
       T_END(T_TERM, t_tm);
 #ifdef EXP_CHECK_NOEXIT  // timing ablation: checks computed, 125 iterations regardless
       if (iter > 100) break;
@@ -1315,12 +1322,12 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   if (!can_check) {
     iter = iter - 1;
     compute_residuals(p, S, R, sb, v, lane TACC_ARG);
-    status = check_termination(p, S, R, dy, dx, sb, v, lane, false);
+    status = check_termination(p, S, R, dy, dx, sb, v, lane, false TACC_ARG);
     if (status == 0) status = MPCQP_UNSOLVED;
   }
   if (iter > p.s.max_iter) iter = p.s.max_iter;
   if (status == MPCQP_UNSOLVED) {
-    const int st = check_termination(p, S, R, dy, dx, sb, v, lane, true);
+    const int st = check_termination(p, S, R, dy, dx, sb, v, lane, true TACC_ARG);
     status = st ? st : MPCQP_MAX_ITER_REACHED;
   }
 

@@ -15,7 +15,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.environ.get("MPCQP_TIMING_LIB") or os.path.join(REPO, "tools", "libmpcqp_timing.so")
 SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact", "resid", "term", "nchk", "adapt",
-         "scale_finish", "vec_rhs", "vec_diag", "vec_update", "rs_stage", "rs_Ax", "rs_Px", "rs_Aty", "rs_norms"]
+         "scale_finish", "vec_rhs", "vec_diag", "vec_update", "rs_stage", "rs_Ax", "rs_Px", "rs_Aty", "rs_norms", "tm_norms", "tm_pinf", "tm_dinf"]
 
 
 def build(extra=()):
@@ -73,7 +73,7 @@ def run(B=65536, steps=5, warmup=3, nx=20):
                                 "term": t["term"] / max(t["nchk"], 1),
                                 "adapt": t["adapt"] / max(t["nchk"], 1),
                                 "check_total": t["check"] / max(t["nchk"], 1),
-                                **{k: t[k] / max(t["nchk"], 1) for k in SLOTS if k.startswith("rs_")}},
+                                **{k: t[k] / max(t["nchk"], 1) for k in SLOTS if k.startswith(("rs_", "tm_"))}},
            "scale_finish_per_solve": t["scale_finish"] / n_inst,
            "cycles_per_solve_step": {"fwd": t["fwd"] / iters / sched["fwd_steps"],
                                      "bwd": t["bwd"] / iters / sched["bwd_steps"]},
