@@ -473,6 +473,23 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const
 #endif
     }
   }
+  // outputs with more than KMAX terms: the first 64 terms' loads of the first LPF of them go out
+  // with the rest
+  constexpr int LPF = 2;
+  double lv[LPF];
+  uint32_t li[LPF];
+#pragma unroll
+  for (int L = 0; L < LPF; ++L) {
+    lv[L] = 0.0, li[L] = 0;
+    if (L < e.nlong && lane < e.long_cnt[L]) {
+      const int q = e.long_off[L] + lane;
+#ifdef EXP_CHKNOLOAD
+      lv[L] = 1e-3, li[L] = (uint32_t)((q + lane) & 63);
+#else
+      lv[L] = val[q], li[L] = e.in[q];
+#endif
+    }
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     double s = 0.0;
@@ -485,12 +502,23 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const
     }
     out[r] = s;
   }
-  // outputs with more than KMAX terms: wave-cooperative sums
+  // long outputs: wave-cooperative sums
   for (int L = 0; L < e.nlong; ++L) {
     double s = 0.0;
-    for (int t = lane; t < e.long_cnt[L]; t += 64) {
+    int t0 = lane;
+#pragma unroll
+    for (int k = 0; k < LPF; ++k)
+      if (k == L) {
+        if (lane < e.long_cnt[L]) s += lv[k] * in[li[k]];
+        t0 = lane + 64;
+      }
+    for (int t = t0; t < e.long_cnt[L]; t += 64) {
       const int q = e.long_off[L] + t;
+#ifdef EXP_CHKNOLOAD  // timing experiment: no global loads in the long outputs
+      s += 1e-3 * in[(q + lane) & 63];
+#else
       s += val[q] * in[e.in[q]];
+#endif
     }
     s = wave_sum(s);
     const int o = e.long_out[L];
@@ -740,7 +768,8 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
 
 template <int RN, int RM>
 __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, RM>& S, double (&dy)[RM],
-                                     const Slab& sb, double* v, int lane, double eps) {
+                                     const Slab& sb, const double (&Ev)[RM], double* v, int lane,
+                                     double eps) {
   const DevPlan& P = p.pl;
   const double thr = OSQP_INFTY * MIN_SCALING;
   double nrm = 0.0;
@@ -752,7 +781,7 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
         dy[r] = (S.l[r] < -thr) ? 0.0 : dmind(dy[r], 0.0);
       else if (S.l[r] < -thr)
         dy[r] = dmaxd(dy[r], 0.0);
-      nrm = dmaxd(nrm, fabs(sb.E[i] * dy[r]));
+      nrm = dmaxd(nrm, fabs(Ev[r] * dy[r]));
     }
   }
   nrm = wave_max(nrm);
@@ -783,7 +812,8 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
 
 template <int RN, int RM>
 __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM>& S, const double (&dx)[RN],
-                                   const Slab& sb, double* v, int lane, double eps) {
+                                   const Slab& sb, const double (&Dv)[RN], double* v, int lane,
+                                   double eps) {
   const DevPlan& P = p.pl;
   const double thr = OSQP_INFTY * MIN_SCALING;
   double nrm = 0.0, qdx = 0.0;
@@ -791,7 +821,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
     if (j < P.n) {
-      nrm = dmaxd(nrm, fabs(sb.D[j] * dx[r]));
+      nrm = dmaxd(nrm, fabs(Dv[r] * dx[r]));
       qdx += S.q[r] * dx[r];
     }
   }
@@ -832,6 +862,26 @@ __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>&
                                  double* v, int lane, bool approximate TACC_PARAM) {
   T_BEGIN(t_m0);
   const DevPlan& P = p.pl;
+  // the scalings D, E of the infeasibility certificates: loaded first, in flight under the norms
+  double Ev[RM], Dv[RN];
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int i = lane + 64 * r;
+#ifdef EXP_CHKNOLOAD
+    Ev[r] = 1.0;
+#else
+    Ev[r] = i < P.m ? sb.E[i] : 0.0;
+#endif
+  }
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+#ifdef EXP_CHKNOLOAD
+    Dv[r] = 1.0;
+#else
+    Dv[r] = j < P.n ? sb.D[j] : 0.0;
+#endif
+  }
   double eps_abs = p.s.eps_abs, eps_rel = p.s.eps_rel;
   double eps_pinf = p.s.eps_prim_inf, eps_dinf = p.s.eps_dual_inf;
   if (approximate) eps_abs *= 10, eps_rel *= 10, eps_pinf *= 10, eps_dinf *= 10;
@@ -867,13 +917,13 @@ __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>&
   if (S.pri_res < eps_prim)
     prim_ok = true;
   else
-    prim_inf = is_primal_infeasible(p, S, dy, sb, v, lane, eps_pinf);
+    prim_inf = is_primal_infeasible(p, S, dy, sb, Ev, v, lane, eps_pinf);
   T_END(T_TM1, t_m1);
   T_BEGIN(t_m2);
   if (S.dua_res < eps_dual)
     dual_ok = true;
   else
-    dual_inf = is_dual_infeasible(p, S, dx, sb, v, lane, eps_dinf);
+    dual_inf = is_dual_infeasible(p, S, dx, sb, Dv, v, lane, eps_dinf);
   T_END(T_TM2, t_m2);
   if (prim_ok && dual_ok) return approximate ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED;
   if (prim_inf) return approximate ? MPCQP_PRIMAL_INFEASIBLE_INACCURATE : MPCQP_PRIMAL_INFEASIBLE;
