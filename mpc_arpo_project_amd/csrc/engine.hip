@@ -202,9 +202,21 @@ __device__ __forceinline__ void load_solve(Rsrc rs, int soff, uint32_t lane, Sol
     const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + q * 1024, soff, 0);
     r.a[2 * q] = w[0], r.b[2 * q] = w[1], r.a[2 * q + 1] = w[2], r.b[2 * q + 1] = w[3];
   }
+#ifdef EXP_FOUR_LOADS  // timing experiment: no target load (targets = valid, aligned operand slots of
+  // the same record, masked as a packed format would; wrong numerics, fixed-work timing only)
+  // per-lane distinct, aligned slots at the image start (conflict-free like real targets)
+  r.t0 = (r.a[1] & 0xff000000u) | (lane * 8u), r.t1 = r.t0;
+  r.t2 = (r.a[5] & 0xff000000u) | (lane * 8u + 512u), r.t3 = (r.a[7] & 0xff000000u) | (lane * 8u + 1024u);
+  r.a[0] &= 0xffffu, r.a[2] &= 0xffffu, r.a[4] &= 0xffffu;
+#else
   const auto tg =
       __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + 4 * SOLVE_TERM_WORDS, soff, 0);
   r.t0 = tg[0], r.t1 = tg[1], r.t2 = tg[2], r.t3 = tg[3];
+#ifdef EXP_TGT_LANE  // timing experiment: the loaded targets replaced by conflict-free lane slots
+  r.t0 = (r.t0 & 0xff000000u) | (lane * 8u), r.t1 = r.t0;
+  r.t2 = (r.t2 & 0xff000000u) | (lane * 8u + 512u), r.t3 = (r.t3 & 0xff000000u) | (lane * 8u + 1024u);
+#endif
+#endif
 }
 // one lane's records of a factorization step: meta word + FAC_MAXC (a, b, c, -) address quads
 struct FacRec {
