@@ -57,3 +57,32 @@ def test_layout_optimiser_lowers_modelled_lds_cycles(monkeypatch):
     tot = lambda d: d["read"] + d["atomic"] + d["vec"]
     assert opt["floor"] == greedy["floor"] == 13 * 44 + 6 * 10
     assert tot(opt) < 0.8 * tot(greedy), (opt, greedy)
+
+
+@pytest.mark.parametrize("paired", ["0", "1"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_emulated_schedule_random_structures(monkeypatch, paired, seed):
+    """both step kinds (paired: segments 0 + 1 of a lane on one target, 3 atomics; unpaired: 4)
+    solve the KKT system of random sparse QPs, not only the MPC structure the planner was tuned on"""
+    monkeypatch.setenv("MPCQP_PAIRED", paired)
+    rng = np.random.default_rng(100 + seed)
+    n, m = 70 + 13 * seed, 110 + 17 * seed
+    # within the residual layout's widths (rows of A <= 8 terms, symmetric rows of P <= 4)
+    off = rng.uniform(-0.3, 0.3, n - 1)
+    P = sp.diags([off, 2.0 + rng.random(n), off], [-1, 0, 1], format="csc")
+    rows, cols = [], []
+    for i in range(m):
+        for j in rng.choice(n, size=int(rng.integers(2, 6)), replace=False):
+            rows.append(i), cols.append(int(j))
+    A = sp.csc_matrix((rng.standard_normal(len(rows)), (rows, cols)), shape=(m, n))
+    P, A = triu_csc(P), sorted_csc(A)
+    rho = 10.0 ** rng.uniform(-2, 2, m)
+    sigma = 1e-6
+    rhs = rng.standard_normal(n + m)
+    sol, model = _lib.schedule_check(P, A, sigma, rho, rhs)
+    K = _kkt(P + sp.triu(P, 1).T, A, sigma, rho)
+    ref = sp.linalg.spsolve(K, rhs)
+    rel = np.abs(sol - ref).max() / np.abs(ref).max()
+    res = np.abs(K @ sol - rhs).max() / np.abs(rhs).max()
+    assert rel < 1e-8 and res < 1e-9, (rel, res)
+    assert model["floor"] > 0
