@@ -1214,9 +1214,17 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   // past the end of x or z have their own W padding slot, zeroed every iteration and read back as 0
   int wsx[RN], wsz[RM];
 #pragma unroll
+#ifdef EXP_VEC_CONTIG  // timing experiment: register-order W slots (conflict-free passes; wrong numerics)
+  for (int r = 0; r < RN; ++r) wsx[r] = P.W + lane + 64 * r;
+#else
   for (int r = 0; r < RN; ++r) wsx[r] = (int)P.wsx[lane + 64 * r];
+#endif
 #pragma unroll
+#ifdef EXP_VEC_CONTIG
+  for (int r = 0; r < RM; ++r) wsz[r] = P.W + lane + 64 * (RN + r);
+#else
   for (int r = 0; r < RM; ++r) wsz[r] = (int)P.wsz[lane + 64 * r];
+#endif
   const int coff = P.CACC - P.W;  // rhs goes to the accumulator region, the solution comes back in W
   const uint32_t wcp = P.wcopy[lane];
   // loop constants held in VGPRs (an opaque copy: otherwise they are re-read from the kernel
