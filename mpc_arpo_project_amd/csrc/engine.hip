@@ -202,21 +202,9 @@ __device__ __forceinline__ void load_solve(Rsrc rs, int soff, uint32_t lane, Sol
     const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + q * 1024, soff, 0);
     r.a[2 * q] = w[0], r.b[2 * q] = w[1], r.a[2 * q + 1] = w[2], r.b[2 * q + 1] = w[3];
   }
-#ifdef EXP_FOUR_LOADS  // timing experiment: no target load (targets = valid, aligned operand slots of
-  // the same record, masked as a packed format would; wrong numerics, fixed-work timing only)
-  // per-lane distinct, aligned slots at the image start (conflict-free like real targets)
-  r.t0 = (r.a[1] & 0xff000000u) | (lane * 8u), r.t1 = r.t0;
-  r.t2 = (r.a[5] & 0xff000000u) | (lane * 8u + 512u), r.t3 = (r.a[7] & 0xff000000u) | (lane * 8u + 1024u);
-  r.a[0] &= 0xffffu, r.a[2] &= 0xffffu, r.a[4] &= 0xffffu;
-#else
   const auto tg =
       __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + 4 * SOLVE_TERM_WORDS, soff, 0);
   r.t0 = tg[0], r.t1 = tg[1], r.t2 = tg[2], r.t3 = tg[3];
-#ifdef EXP_TGT_LANE  // timing experiment: the loaded targets replaced by conflict-free lane slots
-  r.t0 = (r.t0 & 0xff000000u) | (lane * 8u), r.t1 = r.t0;
-  r.t2 = (r.t2 & 0xff000000u) | (lane * 8u + 512u), r.t3 = (r.t3 & 0xff000000u) | (lane * 8u + 1024u);
-#endif
-#endif
 }
 // one lane's records of a factorization step: meta word + FAC_MAXC (a, b, c, -) address quads
 struct FacRec {
@@ -268,40 +256,13 @@ template <bool PAIRED>
 __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
   double x[8], y[8];
 #pragma unroll
-#ifdef EXP_NO_LDSREAD  // timing ablation: operands from the record words instead of LDS
-  for (int c = 0; c < 8; ++c) x[c] = (double)r.a[c], y[c] = (double)r.b[c];
-#elif defined(EXP_NO_MATREAD)  // timing ablation: matrix operands not read from LDS
-  for (int c = 0; c < 8; ++c) x[c] = (double)r.a[c], y[c] = lds_ld(v, r.b[c]);
-#else
   for (int c = 0; c < 8; ++c) x[c] = lds_ld(v, r.a[c]), y[c] = lds_ld(v, r.b[c]);
-#endif
   __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
   __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
   const double n0 = fma(-x[1], y[1], -(x[0] * y[0]));
   const double n1 = fma(-x[3], y[3], -(x[2] * y[2]));
   const double n2 = fma(-x[5], y[5], -(x[4] * y[4]));
   const double n3 = fma(-x[7], y[7], -(x[6] * y[6]));
-#if defined(EXP_WRITE_NOT_ADD)  // timing ablation: plain stores instead of LDS atomics
-  lds_st(v, r.t0, n0 + n1);
-  lds_st(v, r.t2, n2);
-  lds_st(v, r.t3, n3);
-#elif defined(EXP_NO_ATOMIC)  // timing ablation: no LDS writes at all (keeps the values live)
-  asm volatile("" ::"v"(n0), "v"(n1), "v"(n2), "v"(n3));
-#elif defined(EXP_MASKED_ADDS)  // timing ablation: atomics 1-3 issued with EXP_MASKED_ADDS lanes
-  lds_add(r.t0, n0);
-  if (__lane_id() < EXP_MASKED_ADDS) {
-    lds_add(r.t2, n1 + n2);
-    lds_add(r.t3, n3);
-  }
-#elif defined(EXP_SEQ01)  // diagnostic: the pair added as two atomics (the old rounding)
-  lds_add(r.t0, n0);
-  lds_add(r.t0, n1);
-  lds_add(r.t2, n2);
-  lds_add(r.t3, n3);
-#elif defined(EXP_TWO_ADDS)  // timing ablation: two atomics per lane
-  lds_add(r.t0, n0 + n1);
-  lds_add(r.t2, n2 + n3);
-#else
   if constexpr (PAIRED) {
     // segments 0 and 1 are a pair of one target (or segment 1 is unused: its zero-padding terms
     // give -0, and n0 + -0 == n0 exactly) -- one atomic for both
@@ -312,7 +273,6 @@ __device__ __forceinline__ void solve_step(const SolveRec& r, double* v) {
   }
   lds_add(r.t2, n2);
   lds_add(r.t3, n3);
-#endif
   LDS_FENCE();
 }
 // One factorization step: v[t] <- -sum_c v[a_c] v[b_c] v[c_c]; a D_j task (in place on the 1/D slot,
@@ -331,8 +291,6 @@ __device__ __forceinline__ void fac_step(const FacRec& r, double* v) {
   LDS_FENCE();
 }
 
-// Step loops.  Records (L2-resident, fixed stride) rotate through three register sets, so the
-// records of step s + 2 are in flight while steps s and s + 1 compute.
 // Step loops.  Records (L2-resident, fixed stride) rotate through three register sets, so the
 // records of step s + 2 are in flight while steps s and s + 1 compute.  prefetch() issues the
 // first three steps' loads; callers issue it ahead of unrelated work to hide the L2 latency.
@@ -360,18 +318,12 @@ __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops
 // The rotation is unrolled 12 steps deep: LLVM's waitcnt insertion merges states pessimistically
 // at a loop header (the first step after it would wait for all three sets), so the header is
 // reached at most once per ~12 steps.
-#ifdef EXP_NO_RECLOAD  // timing ablation: the three prefetched record sets are reused
-#define MPCQP_STEP(X)                                       \
-  ops.step(p.X, s);                                         \
-  if (++s >= n) break;
-#else
 #define MPCQP_STEP(X)                                       \
   ops.step(p.X, s);                                         \
   if (++s >= n) break;                                      \
   __builtin_amdgcn_sched_barrier(0);                        \
   Ops::load(rs, step_off<Ops>(n, s + 2), lane, p.X);        \
   __builtin_amdgcn_sched_barrier(0);
-#endif
 template <typename Ops>
 __device__ __forceinline__ void run_body(Rsrc rs, int n, uint32_t lane, const Ops& ops,
                                          Pipe<Ops>& p) {
@@ -473,16 +425,8 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       const int t = e.off[r] + 64 * k + lane;
-#ifdef EXP_NOVAL  // timing experiment: no value loads
-      a[r][k] = 1e-3 * (k + 1);
-#else
       a[r][k] = val[t];
-#endif
-#ifdef EXP_NOIDX  // timing experiment: no index loads
-      ix[r][k] = (uint32_t)((lane + 7 * k) & 63);
-#else
       ix[r][k] = e.in[t];
-#endif
     }
   }
   // outputs with more than KMAX terms: the first 64 terms' loads of the first LPF of them go out
@@ -495,11 +439,7 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const
     lv[L] = 0.0, li[L] = 0;
     if (L < e.nlong && lane < e.long_cnt[L]) {
       const int q = e.long_off[L] + lane;
-#ifdef EXP_CHKNOLOAD
-      lv[L] = 1e-3, li[L] = (uint32_t)((q + lane) & 63);
-#else
       lv[L] = val[q], li[L] = e.in[q];
-#endif
     }
   }
 #pragma unroll
@@ -526,11 +466,7 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const
       }
     for (int t = t0; t < e.long_cnt[L]; t += 64) {
       const int q = e.long_off[L] + t;
-#ifdef EXP_CHKNOLOAD  // timing experiment: no global loads in the long outputs
-      s += 1e-3 * in[(q + lane) & 63];
-#else
       s += val[q] * in[e.in[q]];
-#endif
     }
     s = wave_sum(s);
     const int o = e.long_out[L];
@@ -708,9 +644,7 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
     if (i < P.m) v[P.slotRho[i]] = -rinv_of(S, r);
   }
   LDS_FENCE();
-#ifndef EXP_SKIP_FACTOR  // timing ablation
   run_factor(p, v, lane);
-#endif
 }
 
 // update_info: scaled Ax, Px, A'y and the unscaled residual norms (auxil.c compute_pri_res /
@@ -741,11 +675,7 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   for (int r = 0; r < RM; ++r) yb[lane + 64 * r] = S.y[r];
   LDS_FENCE();
   double pr = 0.0, dr = 0.0;
-#ifdef EXP_SLAB0  // timing experiment: every wave reads wave 0's (L2-resident) matrix values
-  const Slab sbv = slab_of(P, p.scratch);
-#else
   const Slab& sbv = sb;
-#endif
   T_END(T_RS0, t_r0);
   T_BEGIN(t_r1);
   ell_mv<RM, ELL_KA>(P.eA, sbv.vA, xb, R.Ax, lane);  // padding terms are 0 * x
@@ -879,20 +809,12 @@ __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>&
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
-#ifdef EXP_CHKNOLOAD
-    Ev[r] = 1.0;
-#else
     Ev[r] = i < P.m ? sb.E[i] : 0.0;
-#endif
   }
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
-#ifdef EXP_CHKNOLOAD
-    Dv[r] = 1.0;
-#else
     Dv[r] = j < P.n ? sb.D[j] : 0.0;
-#endif
   }
   double eps_abs = p.s.eps_abs, eps_rel = p.s.eps_rel;
   double eps_pinf = p.s.eps_prim_inf, eps_dinf = p.s.eps_dual_inf;
@@ -1030,11 +952,7 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
   double cprev = 1.0;  // cost factor of the last pass, not yet applied to P's values
   double dpc[RN];      // P's column norms before that factor (the cost normalisation's)
   LDS_FENCE();
-#ifdef EXP_SKIP_SCALE  // timing ablation: no Ruiz passes
-  for (int it = 0; it < 0; ++it) {
-#else
   for (int it = 0; it < p.s.scaling; ++it) {
-#endif
     // compute_inf_norm_cols_KKT: columns of [P A'; A 0] (P symmetric from its upper triangle).
     // After the first pass P's column norms are the cost normalisation's norms times its factor
     // c (still pending on P's values): max_k |c x_k| = c max_k |x_k| exactly, rounding being
@@ -1214,17 +1132,9 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   // past the end of x or z have their own W padding slot, zeroed every iteration and read back as 0
   int wsx[RN], wsz[RM];
 #pragma unroll
-#ifdef EXP_VEC_CONTIG  // timing experiment: register-order W slots (conflict-free passes; wrong numerics)
-  for (int r = 0; r < RN; ++r) wsx[r] = P.W + lane + 64 * r;
-#else
   for (int r = 0; r < RN; ++r) wsx[r] = (int)P.wsx[lane + 64 * r];
-#endif
 #pragma unroll
-#ifdef EXP_VEC_CONTIG
-  for (int r = 0; r < RM; ++r) wsz[r] = P.W + lane + 64 * (RN + r);
-#else
   for (int r = 0; r < RM; ++r) wsz[r] = (int)P.wsz[lane + 64 * r];
-#endif
   const int coff = P.CACC - P.W;  // rhs goes to the accumulator region, the solution comes back in W
   const uint32_t wcp = P.wcopy[lane];
   // loop constants held in VGPRs (an opaque copy: otherwise they are re-read from the kernel
@@ -1251,7 +1161,6 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     double xp[RN], zp[RM], bz[RM];
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
     // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
-#ifndef EXP_SKIP_RHS  // timing ablations (tools/ablate_fixed.sh): EXP_NOCHECK + EXP_SKIP_*
     // The forward solve accumulates into W, which starts at 0 except on the copy rows (first
     // block, empty reach: W_r = rhs_r, no solve task); the lanes' slots cover all of W
 #pragma unroll
@@ -1268,23 +1177,14 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       v[wsz[r] + coff] = bz[r];
       v[wsz[r]] = (wcp >> (RN + r)) & 1u ? bz[r] : 0.0;
     }
-#else
-#pragma unroll
-    for (int r = 0; r < RN; ++r) xp[r] = S.x[r];
-#pragma unroll
-    for (int r = 0; r < RM; ++r) zp[r] = S.z[r], bz[r] = S.y[r];
-#endif
     LDS_FENCE();
     T_END(T_VEC, t_v0);
     T_END(T_V0, t_v0);
     T_BEGIN(t_fw);
-#ifndef EXP_SKIP_FWD
     run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
-#endif
     T_END(T_FWD, t_fw);
     T_BEGIN(t_v1);
     prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
-#ifndef EXP_SKIP_DIAG
     {
       double wv[RN + RM], dv[RN + RM];
 #pragma unroll
@@ -1298,34 +1198,23 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         v[P.W + lane + 64 * r] = 0.0;
       }
     }
-#endif
     LDS_FENCE();
     T_END(T_VEC, t_v1);
     T_END(T_V1, t_v1);
     T_BEGIN(t_bw);
-#ifndef EXP_SKIP_BWD
     run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
-#endif
     T_END(T_BWD, t_bw);
     T_BEGIN(t_v2);
     // x, z, y updates (auxil.c update_x / update_z / update_y)
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
-#ifdef EXP_SKIP_UPDATE
-      const double xt = 0.0;
-#else
       const double xt = v[wsx[r]];  // the junk slot reads back 0
-#endif
       S.x[r] = alpha * xt + alpha_c * xp[r];
       dx[r] = S.x[r] - xp[r];
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
-#ifdef EXP_SKIP_UPDATE
-      const double nu = 0.0;
-#else
       const double nu = v[wsz[r]];
-#endif
       const double ri = rinv_of(S, r);
       const double zt = bz[r] + ri * nu;
       const double zr = alpha * zt + alpha_c * zp[r];
@@ -1341,7 +1230,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     if (can_check) chk_left = chk;
     const bool adapt = ar_int && --ar_left == 0;  // iter % ar_int == 0
     if (adapt) ar_left = ar_int;
-#ifndef EXP_NOCHECK
+#ifndef MPCQP_FIXED_WORK
     if (can_check || adapt) {
       T_BEGIN(t_rs);
       compute_residuals(p, S, R, sb, v, lane TACC_ARG);
@@ -1350,18 +1239,13 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     }
 #endif
     if (can_check) {
-#ifdef EXP_NOCHECK
+#ifdef MPCQP_FIXED_WORK  // diagnostic builds only: 125 iterations per solve, no termination checks
       if (iter > 100) break;
       continue;
 #endif
       T_BEGIN(t_tm);
       status = check_termination(p, S, R, dy, dx, sb, v, lane, false TACC_ARG);
       T_END(T_TERM, t_tm);
-#ifdef EXP_CHECK_NOEXIT  // timing ablation: checks computed, 125 iterations regardless
-      if (iter > 100) break;
-      status = 0;
-      continue;
-#endif
       if (status != 0) break;
       status = MPCQP_UNSOLVED;
     }

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-2 evidence at HEAD (GPU box): default bench with the CPU baseline; rocprofv3 kernel trace of
+# Profile evidence at HEAD (GPU box): default bench with the CPU baseline; rocprofv3 kernel trace of
 # the default workload; PMC passes (FETCH_SIZE / WRITE_SIZE with calibration, SQ LDS counters); the
-# N=40 impulsive delta-v bench (BASELINE config 3) with its kernel trace.   usage: tools/r02_profile.sh <tag>
+# N=40 impulsive delta-v bench (BASELINE config 3) with its kernel trace.   usage: tools/profile.sh <tag>
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-prof}"; mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
