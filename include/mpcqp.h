@@ -157,6 +157,10 @@ int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int
  * triangular solves, LDS bytes per instance and resident waves (instances in flight) per CU. */
 int mpcqp_schedule_info(const mpcqp_handle *h, int32_t *fac_steps, int32_t *fwd_steps,
                         int32_t *bwd_steps, int32_t *lds_bytes, int32_t *waves_per_cu);
+/* Kind of the triangular-solve steps: *atomics_per_step = LDS atomic additions one lane issues per
+ * solve step (3 for paired steps -- segments 0 + 1 of a lane summed into one target -- 4 otherwise).
+ * The bench's LDS byte model reads it. */
+int mpcqp_schedule_kind(const mpcqp_handle *h, int32_t *atomics_per_step);
 /* Which linear-system engine the handle runs (MPCQP_ENGINE_KKT: the only engine of this build;
  * round 1's dense-inverse alternative measured slower and was removed). */
 int mpcqp_engine_kind(const mpcqp_handle *h, int32_t *kind);

@@ -20,7 +20,7 @@ EXPORTED = (
     "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
     "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_get_state", "mpcqp_set_state", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
     "mpcqp_schedule_check",
-    "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind",
+    "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind", "mpcqp_schedule_kind",
     "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
     "mpcqp_cl_set_ids", "mpcqp_cl_set_tracking", "mpcqp_cl_noise", "mpcqp_cl_set_plant", "mpcqp_clc_period",
     "mpcqp_ukf_create", "mpcqp_ukf_destroy", "mpcqp_ukf_step", "mpcqp_plant_rk45",
@@ -115,6 +115,7 @@ def lib():
     L.mpcqp_solve.argtypes = [vp, dp, dp, C.POINTER(Info)]
     L.mpcqp_dims.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
     L.mpcqp_engine_kind.argtypes = [vp, i32p]
+    L.mpcqp_schedule_kind.argtypes = [vp, i32p]
     L.mpcqp_copy_data.argtypes = [vp, dp, dp, dp]
     L.mpcqp_get_state.argtypes = [vp, dp, dp, dp, dp, dp]
     L.mpcqp_set_state.argtypes = [vp, dp, dp, dp, dp, dp]

@@ -400,6 +400,12 @@ class BatchClosedLoopC(BatchClosedLoop):
         self._init_noise(noise, noise_seed, noise_source, xest, noise_dt=prob.T * hold)
         self.period_index = 0
 
+    def enable_tracking(self, nsim, dist_tol=0.2, ang_tol=45.0):
+        """Not available for the continuous loop: mpcqp_clc_period keeps i_term (self.iterm) but
+        not the success / final-error / fallback run summary of the discrete loop's tracking."""
+        raise NotImplementedError("run summaries are tracked by the discrete loop only; "
+                                  "BatchClosedLoopC exposes iterm, done and ctrl_seq")
+
     def _noise_scale(self):
         s = 1.0 / np.sqrt(0.001)
         return self.noise[0] * s, self.noise[0] * s  # Qcont = diag(sig_x^2, sig_x^2) (quirk)
@@ -408,12 +414,16 @@ class BatchClosedLoopC(BatchClosedLoop):
     def periods(self):
         return len(self.schedule)
 
-    def period(self, traj=None):
-        """One sample period for every chaser (async); traj: optional (B, nsub, 4) tensor"""
+    def period(self, traj=None, on_solved=None):
+        """One sample period for every chaser (async); traj: optional (B, nsub, 4) tensor;
+        on_solved(stream): called right after the solve is enqueued (e.g. an event record, to
+        split the period's time between the solve and the plant / UKF / configure work)"""
         if self.period_index >= len(self.schedule):
             raise MPCQPError("the simulation horizon is exhausted")
         i0, nsub, t0 = self.schedule[self.period_index]
         r = self.qp.solve_async()
+        if on_solved is not None:
+            on_solved(self.qp.stream)
         L = _lib.lib()
         opt = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         if traj is not None and (tuple(traj.shape) != (self.B, nsub, 4) or

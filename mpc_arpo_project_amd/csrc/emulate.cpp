@@ -6,6 +6,7 @@
 // compiled (and the layout optimiser rewrote) still solves the KKT system; the product never runs
 // it.  Slots nobody initialises hold NaN, so a schedule that reads a stale slot shows up as NaN.
 #include <cmath>
+#include <cstring>
 #include <cstdint>
 #include <limits>
 #include <vector>
@@ -114,13 +115,21 @@ bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, doubl
     v[pl.wsz[i] + coff] = b;
     v[pl.wsz[i]] = (pl.wcopy[i % 64] >> (pl.RN + i / 64)) & 1u ? b : 0.0;
   }
+  // the solves' idle segments add -0.0 to sink slots in the 1/D region: every 1/D slot must come
+  // out of the solve tables bit-identical (a non-zero "idle" product would corrupt a live 1/D_j)
+  const std::vector<double> dinv(v.begin() + pl.DINV, v.begin() + pl.DINV + pl.NKP);
+  auto dinv_intact = [&]() {
+    return std::memcmp(dinv.data(), v.data() + pl.DINV, sizeof(double) * pl.NKP) == 0;
+  };
   run_solve_table(pl.fwd, pl.nfwd, pl.paired, v);
+  bool intact = dinv_intact();
   for (int k = 0; k < pl.NKP; ++k) {
     v[pl.CACC + k] = v[pl.W + k] * v[pl.DINV + k];
     v[pl.W + k] = 0.0;
   }
   run_solve_table(pl.bwd, pl.nbwd, pl.paired, v);
-  bool finite = true;
+  intact = intact && dinv_intact();
+  bool finite = intact;
   for (int j = 0; j < n; ++j) sol[j] = v[pl.wsx[j]], finite = finite && std::isfinite(sol[j]);
   for (int i = 0; i < m; ++i) sol[n + i] = v[pl.wsz[i]], finite = finite && std::isfinite(sol[n + i]);
   // the padding lanes' slots read back 0 (the kernel relies on it)

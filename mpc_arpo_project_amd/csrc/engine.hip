@@ -300,7 +300,12 @@ struct Pipe {
 };
 template <typename Ops>
 __device__ __forceinline__ int step_off(int n, int s) {
+#ifdef MPCQP_OOR_TAIL
+  (void)n;
+  return s * (Ops::STRIDE * 4);  // past the table: the buffer's range check returns zeros
+#else
   return (s < n ? s : n - 1) * (Ops::STRIDE * 4);
+#endif
 }
 template <typename Ops>
 __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops>& p) {
@@ -1135,7 +1140,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   for (int r = 0; r < RN; ++r) wsx[r] = (int)P.wsx[lane + 64 * r];
 #pragma unroll
   for (int r = 0; r < RM; ++r) wsz[r] = (int)P.wsz[lane + 64 * r];
-  const int coff = P.CACC - P.W;  // rhs goes to the accumulator region, the solution comes back in W
+  // rhs goes to the accumulator region C, the solution comes back in W; C follows W at a distance
+  // of NKP = 64 (RN + RM) doubles (symbolic.cpp relocate), a compile-time constant: the stores'
+  // immediate offset, so no second address register per slot
+  constexpr int coff = 64 * (RN + RM);
   const uint32_t wcp = P.wcopy[lane];
   // loop constants held in VGPRs (an opaque copy: otherwise they are re-read from the kernel
   // arguments inside the loop, with an lgkmcnt(0) wait that also drains the LDS queue)
@@ -1154,28 +1162,40 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   const SolveOps<PAIRED> sops{v};
   const Rsrc rs_fwd = table_rsrc(P.fwd, P.nfwd, SOLVE_STEP_WORDS);
   const Rsrc rs_bwd = table_rsrc(P.bwd, P.nbwd, SOLVE_STEP_WORDS);
+#ifdef MPCQP_EARLY_FWD
+  bool fwd_ready = false;
+#endif
   for (iter = 1; iter <= p.s.max_iter; ++iter) {
     T_COUNT(T_ITERS);
     T_BEGIN(t_v0);
+#ifdef MPCQP_EARLY_FWD
+    if (!fwd_ready) prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);
+    fwd_ready = false;
+#else
     prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);  // lands while the right-hand side is formed
+#endif
     double xp[RN], zp[RM], bz[RM];
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
     // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
     // The forward solve accumulates into W, which starts at 0 except on the copy rows (first
     // block, empty reach: W_r = rhs_r, no solve task); the lanes' slots cover all of W
+    uint32_t wcpi = wcp;  // re-derived every iteration (no hoisted per-slot lane masks)
+#ifndef LV_NOWCP
+    asm volatile("" : "+v"(wcpi));
+#endif
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       xp[r] = S.x[r];
       const double b = sigma * xp[r] - S.q[r];
       v[wsx[r] + coff] = b;
-      v[wsx[r]] = (wcp >> r) & 1u ? b : 0.0;
+      v[wsx[r]] = (wcpi >> r) & 1u ? b : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       zp[r] = S.z[r];
       bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
       v[wsz[r] + coff] = bz[r];
-      v[wsz[r]] = (wcp >> (RN + r)) & 1u ? bz[r] : 0.0;
+      v[wsz[r]] = (wcpi >> (RN + r)) & 1u ? bz[r] : 0.0;
     }
     LDS_FENCE();
     T_END(T_VEC, t_v0);
@@ -1205,6 +1225,12 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
     T_END(T_BWD, t_bw);
     T_BEGIN(t_v2);
+#ifdef MPCQP_EARLY_FWD
+    if (chk_left != 1 && ar_left != 1) {  // no check / rho adaptation after this iteration
+      prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);
+      fwd_ready = true;
+    }
+#endif
     // x, z, y updates (auxil.c update_x / update_z / update_y)
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
@@ -1230,10 +1256,16 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     if (can_check) chk_left = chk;
     const bool adapt = ar_int && --ar_left == 0;  // iter % ar_int == 0
     if (adapt) ar_left = ar_int;
+    // check-time code gets an opaque copy of the lane id: its per-lane addresses are recomputed at
+    // each check instead of being hoisted out of the ADMM loop into registers
+    int clane = lane;
+#ifndef LV_NOCLANE
+    asm volatile("" : "+v"(clane));
+#endif
 #ifndef MPCQP_FIXED_WORK
     if (can_check || adapt) {
       T_BEGIN(t_rs);
-      compute_residuals(p, S, R, sb, v, lane TACC_ARG);
+      compute_residuals(p, S, R, sb, v, clane TACC_ARG);
       T_END(T_RESID, t_rs);
       T_COUNT(T_NCHK);
     }
@@ -1244,14 +1276,14 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       continue;
 #endif
       T_BEGIN(t_tm);
-      status = check_termination(p, S, R, dy, dx, sb, v, lane, false TACC_ARG);
+      status = check_termination(p, S, R, dy, dx, sb, v, clane, false TACC_ARG);
       T_END(T_TERM, t_tm);
       if (status != 0) break;
       status = MPCQP_UNSOLVED;
     }
     T_BEGIN(t_ad);
     if (adapt) {
-      const double rho_new = rho_estimate(p, S, R, lane);
+      const double rho_new = rho_estimate(p, S, R, clane);
       if (rho_new > S.rho * p.s.adaptive_rho_tolerance ||
           rho_new < S.rho / p.s.adaptive_rho_tolerance) {
         S.rho = dmind(dmaxd(rho_new, RHO_MIN), RHO_MAX);
@@ -1259,7 +1291,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         rho_updates++;
         LDS_FENCE();
         T_BEGIN(t_f1);
-        assemble_and_factor<RN, RM>(p, sb, v, lane, S);
+        assemble_and_factor<RN, RM>(p, sb, v, clane, S);
 #ifdef MPCQP_TIMING
         const unsigned long long dt_f1 = __builtin_amdgcn_s_memtime() - t_f1;
         tacc[T_FACTOR] += dt_f1;
@@ -1367,7 +1399,14 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
     inst = __builtin_amdgcn_readfirstlane(inst);
     if (inst >= (unsigned int)p.B) break;
     if (p.skip && p.skip[inst]) continue;  // wave-uniform
-    solve_instance<RN, RM, PAIRED>(p, (int)inst, v, scr, lane);
+    // an opaque copy of the lane id per instance: per-lane address arithmetic cannot be hoisted
+    // out of the instance loop (held in registers for the whole kernel, it would cost the
+    // solve loop its occupancy)
+    int ilane = lane;
+#ifndef LV_NOILANE
+    asm volatile("" : "+v"(ilane));
+#endif
+    solve_instance<RN, RM, PAIRED>(p, (int)inst, v, scr, ilane);
     LDS_FENCE();
   }
 }
@@ -1506,6 +1545,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     return fail(MPCQP_E_UNSUPPORTED, e);
   }
   const Plan& pl = h->plan;
+  if (pl.CACC - pl.W != pl.NKP) {  // the kernel addresses C as W + NKP (an immediate offset)
+    delete h;
+    return fail(MPCQP_E_UNSUPPORTED, "internal: accumulator region does not follow the solve vector");
+  }
   if (pl.nfac < 1 || pl.nfwd < 1 || pl.nbwd < 1) {
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, "internal: empty schedule");
@@ -1801,6 +1844,12 @@ int mpcqp_schedule_info(const mpcqp_handle* h, int32_t* fac, int32_t* fwd, int32
   return 0;
 }
 
+int mpcqp_schedule_kind(const mpcqp_handle* h, int32_t* atomics_per_step) {
+  if (!h || !atomics_per_step) return fail(MPCQP_E_INVALID, "null argument");
+  *atomics_per_step = h->plan.paired ? 3 : 4;
+  return 0;
+}
+
 int mpcqp_engine_kind(const mpcqp_handle* h, int32_t* kind) {
   if (!h || !kind) return fail(MPCQP_E_INVALID, "null argument");
   *kind = MPCQP_ENGINE_KKT;
@@ -1841,7 +1890,7 @@ int mpcqp_schedule_check(const mpcqp_structure* st, const double* Px, const doub
     model[0] = md.read, model[1] = md.atomic, model[2] = md.vec, model[3] = md.floor;
   }
   if (!emulate_kkt_solve(pl, Px, Ax, sigma, rho_vec, rhs, sol))
-    return fail(MPCQP_E_INVALID, "schedule emulation produced a non-finite or unzeroed slot");
+    return fail(MPCQP_E_INVALID, "schedule emulation produced a non-finite or unzeroed slot, or changed a 1/D slot");
   return 0;
 }
 

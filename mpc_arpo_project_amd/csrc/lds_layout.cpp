@@ -473,8 +473,19 @@ struct Opt {
   void store() {
     const uint32_t zb = (uint32_t)pl.ZERO;
     // zero slot of the least used bank per read group; sinks in free banks per atomic group
+    // sinks: the 1/D region's padding slots (construction slots nk..NKP-1, renamed), which hold 0
+    // and are only ever multiplied by the zero W padding; an idle segment adds -0.0 (exact no-op).
+    // Should the padding not cover every bank, the live 1/D slots of the missing banks join the
+    // pool (still exact: adding -0.0 never changes a value)
     std::vector<int> sinkpool[WBANKS];
-    for (int k = 0; k < pl.NKP; ++k) sinkpool[(pl.DINV + k) & (WBANKS - 1)].push_back(pl.DINV + k);
+    for (int k = pl.nk; k < pl.NKP; ++k) {
+      const int slot = ren[pl.DINV + k];
+      sinkpool[slot & (WBANKS - 1)].push_back(slot);
+    }
+    for (int k = 0; k < pl.NKP; ++k) {
+      const int slot = ren[pl.DINV + k];
+      if (sinkpool[slot & (WBANKS - 1)].empty()) sinkpool[slot & (WBANKS - 1)].push_back(slot);
+    }
     size_t si = 0;
     for (int w = 0; w < 2; ++w) {
       auto& t = w ? pl.bwd : pl.fwd;

@@ -18,6 +18,7 @@ from . import _lib
 from ._lib import MPCQPError, check
 
 OSQP_INFTY = 1e30
+MPCQP_UNSOLVED = -10  # OSQP 0.6 status_val of an instance no solve has touched (include/mpcqp.h)
 
 
 def _require_gpu(device):
@@ -150,15 +151,27 @@ class BatchQP:
             keep["Ax"] = Ax
         self._keep(**keep)
 
+    def _on_stream(self, fn, *tensors):
+        """run fn (an ABI call that queues copies on the handle's stream) into freshly allocated
+        tensors, then order the caller's current stream after it, so the returned tensors are
+        safe to use on the current stream whatever stream the handle runs on"""
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)  # the allocations happened on the current stream
+        fn()
+        for t in tensors:
+            t.record_stream(self.stream)
+        cur.wait_stream(self.stream)
+        return tensors
+
     def copy_data(self):
-        """(Ax, l, u) currently held by the handle, as new device tensors."""
+        """(Ax, l, u) currently held by the handle, as new device tensors (ordered after the
+        handle's stream for the caller's current stream)."""
         f = dict(dtype=torch.float64, device=self.device)
         Ax = torch.empty(self.B, self.nnzA, **f)
         l = torch.empty(self.B, self.m, **f)
         u = torch.empty(self.B, self.m, **f)
-        check(_lib.lib().mpcqp_copy_data(self._h, Ax.data_ptr(), l.data_ptr(), u.data_ptr()),
-              "mpcqp_copy_data")
-        return Ax, l, u
+        return self._on_stream(lambda: check(_lib.lib().mpcqp_copy_data(
+            self._h, Ax.data_ptr(), l.data_ptr(), u.data_ptr()), "mpcqp_copy_data"), Ax, l, u)
 
     def set_skip(self, mask):
         """int32 device tensor [B] (kept alive by the handle) or None: instances with a non-zero
@@ -180,8 +193,9 @@ class BatchQP:
         ys = torch.empty(self.B, self.m, **f)
         rho = torch.empty(self.B, **f)
         hs = torch.empty(self.B, dtype=torch.int32, device=self.device)
-        check(_lib.lib().mpcqp_get_state(self._h, xs.data_ptr(), zs.data_ptr(), ys.data_ptr(),
-                                         rho.data_ptr(), hs.data_ptr()), "mpcqp_get_state")
+        self._on_stream(lambda: check(_lib.lib().mpcqp_get_state(
+            self._h, xs.data_ptr(), zs.data_ptr(), ys.data_ptr(), rho.data_ptr(), hs.data_ptr()),
+            "mpcqp_get_state"), xs, zs, ys, rho, hs)
         return dict(x=xs, z=zs, y=ys, rho=rho, has_state=hs)
 
     def set_state(self, x, z, y, rho, has_state):
@@ -199,16 +213,24 @@ class BatchQP:
         y = self._batch_vec(y, self.m, "y")
         check(_lib.lib().mpcqp_warm_start(self._h, x.data_ptr(), y.data_ptr()), "mpcqp_warm_start")
 
-    def _outputs(self):
-        if self._out is None:
+    def new_result(self) -> SolveResult:
+        """Output buffers for solve_async(out=...).  An instance that a skip mask keeps from
+        being solved keeps its previous outputs, so a fresh buffer starts from defined values:
+        status MPCQP_UNSOLVED (-10, OSQP's 'unsolved'), iter 0, x / y / obj / residuals NaN."""
+        with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
+            nan = float("nan")
             f = dict(dtype=torch.float64, device=self.device)
             i = dict(dtype=torch.int32, device=self.device)
-            self._out = SolveResult(
-                x=torch.empty(self.B, self.n, **f), y=torch.empty(self.B, self.m, **f),
-                status=torch.empty(self.B, **i), iter=torch.empty(self.B, **i),
-                rho_updates=torch.empty(self.B, **i), obj_val=torch.empty(self.B, **f),
-                pri_res=torch.empty(self.B, **f), dua_res=torch.empty(self.B, **f),
-                rho=torch.empty(self.B, **f))
+            return SolveResult(
+                x=torch.full((self.B, self.n), nan, **f), y=torch.full((self.B, self.m), nan, **f),
+                status=torch.full((self.B,), MPCQP_UNSOLVED, **i), iter=torch.zeros(self.B, **i),
+                rho_updates=torch.zeros(self.B, **i), obj_val=torch.full((self.B,), nan, **f),
+                pri_res=torch.full((self.B,), nan, **f), dua_res=torch.full((self.B,), nan, **f),
+                rho=torch.full((self.B,), nan, **f))
+
+    def _outputs(self):
+        if self._out is None:
+            self._out = self.new_result()
         return self._out
 
     def solve_async(self, out: SolveResult = None) -> SolveResult:
@@ -232,11 +254,12 @@ class BatchQP:
         v = [C.c_int32() for _ in range(5)]
         check(_lib.lib().mpcqp_schedule_info(self._h, *[C.byref(x) for x in v]),
               "mpcqp_schedule_info")
-        k = C.c_int32()
+        k, at = C.c_int32(), C.c_int32()
         check(_lib.lib().mpcqp_engine_kind(self._h, C.byref(k)), "mpcqp_engine_kind")
+        check(_lib.lib().mpcqp_schedule_kind(self._h, C.byref(at)), "mpcqp_schedule_kind")
         return dict(engine="kkt", fac_steps=v[0].value,
                     fwd_steps=v[1].value, bwd_steps=v[2].value, lds_bytes=v[3].value,
-                    waves_per_cu=v[4].value)
+                    waves_per_cu=v[4].value, atomics_per_step=at.value)
 
     def dims(self):
         v = [C.c_int32() for _ in range(5)]

@@ -24,6 +24,18 @@ condition c under noise stream g:
     (filterpy raises numpy.linalg.LinAlgError there: the reference's run would end with it).
 
     python -m mpc_arpo_project_amd.sweep --scenario radial --seeds 1024 --ics 1024 --gpus 8
+
+The reference's two Monte-Carlo experiments, as sweep modes (one fixed initial condition,
+x0 = (100, 10, 0, 0), MC runs each with its own noise stream; rejecting and non-rejecting runs of
+one MC index share their noise stream, as the reference's seed-123 runs share theirs):
+
+    python -m mpc_arpo_project_amd.sweep --experiment disturb_rej [--mc 100]
+        test/disturbRejComp.py:74-100: Nx = 40, T_final = 150, noise sigma 0.7, noise lengths
+        (1, 10, 20, 30, 50, 70, 100, 150, 200, 250) x {isReject False, True}; per noise length
+        the mean final distance |x(i_term - 1) - xr| of each and dist_ratio = rej / no-rej
+    python -m mpc_arpo_project_amd.sweep --experiment success_rates [--mc 300]
+        test/saved_runs/success_rates_test.py:46-75: Nx = 40, T_final = 300, noise sigma 0.3
+        held 50 samples, isReject = True; the count of isSuccess runs
 """
 from __future__ import annotations
 
@@ -53,9 +65,12 @@ def initial_conditions(scenario: str, n_ics: int, seed: int = 20250328) -> np.nd
     return X
 
 
-def scenario_states(scenario: str, n_seeds: int, n_ics: int, lo: int, hi: int, ic_seed: int):
-    """initial states of global scenario ids [lo, hi) (g = s * n_ics + c -> IC c)"""
-    ics = initial_conditions(scenario, n_ics, ic_seed)
+def scenario_states(scenario: str, n_seeds: int, n_ics: int, lo: int, hi: int, ic_seed: int,
+                    x0=None):
+    """initial states of global scenario ids [lo, hi) (g = s * n_ics + c -> IC c); x0: one fixed
+    initial condition for every scenario (the reference's experiment scripts)"""
+    ics = (initial_conditions(scenario, n_ics, ic_seed) if x0 is None else
+           np.tile(np.asarray(x0, dtype=float), (n_ics, 1)))
     g = np.arange(lo, hi)
     assert hi <= n_seeds * n_ics
     return ics[g % n_ics]
@@ -80,7 +95,7 @@ class Sweep:
 
     def __init__(self, scenario="radial", n_seeds=1, n_ics=1024, Nx=20, noise=(0.3, 0.3, 50),
                  isReject=True, T_final=150.0, rank=0, world=1, device="cuda", shards=2,
-                 ic_seed=20250328, noise_seed=123, eps=1e-3, keep_traj=False):
+                 ic_seed=20250328, noise_seed=123, eps=1e-3, keep_traj=False, x0=None):
         import torch
 
         from .closed_loop import ShardedClosedLoop
@@ -89,7 +104,7 @@ class Sweep:
         self.lo, self.hi = launch.shard_range(self.G, rank, world)
         self.sim, self.prob = build(scenario, Nx, noise, isReject, T_final)
         self.nsim = int(self.sim.T_final / self.sim.time_stp)
-        X = scenario_states(scenario, n_seeds, n_ics, self.lo, self.hi, ic_seed)
+        X = scenario_states(scenario, n_seeds, n_ics, self.lo, self.hi, ic_seed, x0)
         # the reference's default OSQP tolerances (eps_abs = eps_rel = 1e-3) unless asked otherwise
         self.loop = ShardedClosedLoop(self.prob, X, shards=shards, device=device, id_offset=self.lo,
                                       noise=noise, noise_seed=noise_seed, eps_abs=eps, eps_rel=eps)
@@ -139,6 +154,67 @@ def reduce(S: np.ndarray):
                 last_status={int(a): int(b) for a, b in zip(st, cnt)})
 
 
+X0_REF = (100., 10., 0., 0.)  # x0 of test/disturbRejComp.py:37 and success_rates_test.py:37
+NOISE_LENGTHS = (1, 10, 20, 30, 50, 70, 100, 150, 200, 250)  # test/disturbRejComp.py:75
+
+
+def _timed_run(sw, dist, device):
+    import torch
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sw.run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def experiment(name, mc, rank, world, device, dist, shards=2, eps=1e-3, noise_seed=123):
+    """the reference's Monte-Carlo experiments (module docstring); returns rank 0's result dict"""
+    if name == "disturb_rej":
+        settings = [(L, rej) for L in NOISE_LENGTHS for rej in (False, True)]
+        Nx, T_final, sig = 40, 150.0, 0.7
+    elif name == "success_rates":
+        settings = [(50, True)]
+        Nx, T_final, sig = 40, 300.0, 0.3
+    else:
+        raise ValueError(f"unknown experiment {name!r}")
+    rows, secs, solves = [], 0.0, 0.0
+    for L, rej in settings:
+        sw = Sweep("radial", mc, 1, Nx=Nx, noise=(sig, sig, int(L)), isReject=rej, T_final=T_final,
+                   rank=rank, world=world, device=device, shards=shards, eps=eps,
+                   noise_seed=noise_seed, x0=X0_REF)
+        el = _timed_run(sw, dist, device)
+        S = launch.gather_rows(sw.summary(), sw.G, rank, world, dist)
+        sw.close()
+        if rank == 0:
+            Sn = S.cpu().numpy()
+            r = reduce(Sn)
+            rows.append(dict(noise_length=int(L), reject=rej, runs=int(Sn.shape[0]),
+                             success=r["success"], aborted=r["aborted"],
+                             final_err_mean=r["final_err_mean"], i_term_mean=r["i_term_mean"],
+                             seconds=el))
+            secs += el
+            solves += float(Sn[:, FIELDS.index("i_term")].sum())
+    if rank != 0:
+        return None
+    out = dict(experiment=name, n_gpus=world, mc=mc, nx=Nx, t_final=T_final, sigma=sig,
+               eps=eps, x0=list(X0_REF), seconds=secs, solves_per_s=solves / max(secs, 1e-9),
+               settings=rows)
+    if name == "disturb_rej":
+        # dist_ratios[i] = mean final distance with rejection / without (disturbRejComp.py:98-100)
+        by = {(r["noise_length"], r["reject"]): r for r in rows}
+        out["dist_ratios"] = {int(L): by[(L, True)]["final_err_mean"] / by[(L, False)]["final_err_mean"]
+                              for L in NOISE_LENGTHS}
+    else:
+        out["success_count"] = rows[0]["success"]
+        out["success_rate"] = rows[0]["success"] / rows[0]["runs"]
+    return out
+
+
 def main(argv=None):
     argv = sys.argv if argv is None else argv
     ap = argparse.ArgumentParser(prog="python -m mpc_arpo_project_amd.sweep")
@@ -154,6 +230,10 @@ def main(argv=None):
     ap.add_argument("--shards", type=int, default=2)
     ap.add_argument("--traj", action="store_true", help="gather trajectories to rank 0")
     ap.add_argument("--out", default="", help="rank 0 saves the [G, 9] summary (.npy)")
+    ap.add_argument("--experiment", choices=("disturb_rej", "success_rates"), default=None,
+                    help="the reference's Monte-Carlo experiment scripts (module docstring)")
+    ap.add_argument("--mc", type=int, default=0,
+                    help="Monte-Carlo runs per setting (default: the reference's 100 / 300)")
     a = ap.parse_args(argv[1:])
     if a.gpus > 1 and not launch.launched():
         return launch.relaunch(a.gpus, argv, module="mpc_arpo_project_amd.sweep")
@@ -162,21 +242,21 @@ def main(argv=None):
     rank, world, local, device, dist = launch.init("nccl")
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but {world} ranks were launched")
+    if a.experiment:
+        mc = a.mc or (100 if a.experiment == "disturb_rej" else 300)
+        out = experiment(a.experiment, mc, rank, world, device, dist, shards=a.shards, eps=a.eps)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return 0
     noise = None if a.noise == "none" else tuple(float(v) for v in a.noise.split(","))
     if noise is not None:
         noise = (noise[0], noise[1], int(noise[2]))
     sw = Sweep(a.scenario, a.seeds, a.ics, Nx=a.nx, noise=noise, isReject=not a.no_reject,
                T_final=a.tfinal, rank=rank, world=world, device=device, shards=a.shards,
                eps=a.eps, keep_traj=a.traj)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    sw.run()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
+    el = _timed_run(sw, dist, device)
     local_sum = sw.summary()
     S = launch.gather_rows(local_sum, sw.G, rank, world, dist)
     traj = None

@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B of engine builds on one box: default bench (no CPU baseline) with each library, alternating.
+# A/B of engine builds on one box: the default bench (no CPU baseline, no config-3 leg) with each
+# library, alternating.  Extra bench flags in AB_ARGS (e.g. AB_ARGS="--split 1 --steps 10").
 # usage: tools/ab_libs.sh <tag> <rounds> lib1.so lib2.so ...   (paths relative to the repo root)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-ab}"; mkdir -p "$O"; cd "$R"
@@ -7,7 +8,7 @@ N=${2:-1}; shift 2
 for r in $(seq 1 $N); do
   for L in "$@"; do
     tag=$(basename $L .so)
-    MPCQP_LIBRARY=$R/$L timeout -k 10 300 python bench.py --no-cpu-baseline > "$O/${tag}_$r.json" 2> "$O/${tag}_$r.err" || { echo "$tag failed"; tail -5 "$O/${tag}_$r.err"; exit 1; }
-    python -c "import json;d=json.load(open('$O/${tag}_$r.json'));print('$tag', round(d['value']), 'waves/cu', d['schedule']['waves_per_cu'], 'lds', d['schedule']['lds_bytes'], 'kernel ms', round(d['roofline']['kernel_ms_per_launch'],2), 'iters', round(d['admm_iters']['mean'],2), 'cold', round(d['cold']['value']))"
+    MPCQP_LIBRARY=$R/$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-config3 $AB_ARGS > "$O/${tag}_$r.json" 2> "$O/${tag}_$r.err" || { echo "$tag failed"; tail -5 "$O/${tag}_$r.err"; exit 1; }
+    python -c "import json;d=json.load(open('$O/${tag}_$r.json'));print('$tag', round(d['value']), 'waves/cu', d['schedule']['waves_per_cu'], 'lds', d['schedule']['lds_bytes'], 'kernel ms', round(d['roofline']['kernel_ms_per_launch'],2), 'iters', round(d['admm_iters']['mean'],2), 'cold', round(d['cold']['value']), 'cold kernel ms', round(d['cold']['kernel_ms_per_launch'],2))"
   done
 done
