@@ -42,7 +42,7 @@ namespace {
 
 // ------------------------------------------------------------------------------------- device
 struct EllDev {
-  const uint16_t *src, *in;
+  const uint16_t *src, *in, *vpos;
   int K[ELL_MAXR], off[ELL_MAXR];
   int total, nlong;
   int long_out[ELL_MAXLONG], long_off[ELL_MAXLONG], long_cnt[ELL_MAXLONG];
@@ -54,7 +54,6 @@ struct DevPlan {
   const uint16_t* Lcol;    // DINV slot of each L entry's column
   int inst_doubles;        // LDS doubles of the instance image (16-byte aligned)
   const uint16_t *slotP, *slotA, *slotRho, *slotSig, *wsx, *wsz;
-  const uint16_t *posA, *posP;  // CSC entry -> position in the ELL value copies (symbolic.hpp)
   const uint16_t *Ap, *Ai, *Acol, *Arp, *Ark, *Arj, *Pi, *Pcol, *Psp, *Psk, *Pso;
   int n, m, nk, nnzP, nnzA, nnzL;
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
@@ -63,6 +62,7 @@ struct DevPlan {
   const uint32_t* wcopy;  // per lane: register slots holding copy rows (symbolic.hpp Plan::wcopy)
   const uint4* sci_src;
   int SCI, S_ZERO, sci_n16, sci_eP, sci_eAt, sci_eA, sci_ra, sci_ca;
+  int MV, MVZ;  // resident scaled values [P | A] (CSC orders) and their zero slot
 };
 
 struct KParams {
@@ -395,67 +395,58 @@ struct Inst {
   double Dinv[RN], Einv[RM];  // inverse scalings (termination checks), 1 past the end of x / z
 };
 
-// per-wave scratch slab layout (doubles): the scalings D, E (unscaling and the infeasibility
-// certificates) and the scaled matrix values in the residual ELL orders (checks, refactorization).
-// 34 KB at N = 20.
+// per-wave scratch slab (doubles): the scalings D, E of the wave's current instance (the
+// infeasibility certificates and the unscaling of the solution).  The scaled matrix values stay
+// in LDS (Plan::MV).
 struct Slab {
   double *D, *E;
-  double *vA, *vAt, *vP;
 };
-__host__ __device__ __forceinline__ size_t slab_doubles(int n, int m, int eA, int eAt, int eP) {
-  return (size_t)n + m + eA + eAt + eP;
-}
-__device__ __forceinline__ size_t slab_doubles(const DevPlan& P) {
-  return slab_doubles(P.n, P.m, P.eA.total, P.eAt.total, P.eP.total);
-}
+__host__ __device__ __forceinline__ size_t slab_doubles(int n, int m) { return (size_t)n + m; }
+__device__ __forceinline__ size_t slab_doubles(const DevPlan& P) { return slab_doubles(P.n, P.m); }
 __device__ __forceinline__ Slab slab_of(const DevPlan& P, double* scr) {
   Slab s;
   s.D = scr;
   s.E = s.D + P.n;
-  s.vA = s.E + P.m;
-  s.vAt = s.vA + P.eA.total;
-  s.vP = s.vAt + P.eAt.total;
   return s;
 }
-// residual mat-vec out[r] = sum_k val[off_r + 64 k + lane] * in[idx[...]] for every slot r of
-// the instance (terms in order).  All value and index loads are issued before the first use.
+// residual mat-vec out[r] = sum_k v[vpos[t]] * in[in_idx[t]], t = off_r + 64 k + lane, for every
+// slot r of the instance (terms in order): the scaled values are the LDS-resident copy (MV), the
+// two index lists are shared by all instances.  All index loads are issued before the first use.
 template <int R, int KMAX>
-__device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const double* in,
+__device__ __forceinline__ void ell_mv(const EllDev& e, const double* v, const double* in,
                                        double (&out)[R], int lane) {
-  double a[R][KMAX];
-  uint32_t ix[R][KMAX];
+  uint32_t vp[R][KMAX], ix[R][KMAX];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (e.K[r] == 0) continue;  // slot beyond the instance (wave-uniform)
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       const int t = e.off[r] + 64 * k + lane;
-      a[r][k] = val[t];
+      vp[r][k] = e.vpos[t];
       ix[r][k] = e.in[t];
     }
   }
   // outputs with more than KMAX terms: the first 64 terms' loads of the first LPF of them go out
   // with the rest
   constexpr int LPF = 2;
-  double lv[LPF];
-  uint32_t li[LPF];
+  uint32_t lp[LPF], li[LPF];
 #pragma unroll
   for (int L = 0; L < LPF; ++L) {
-    lv[L] = 0.0, li[L] = 0;
+    lp[L] = 0, li[L] = 0;
     if (L < e.nlong && lane < e.long_cnt[L]) {
       const int q = e.long_off[L] + lane;
-      lv[L] = val[q], li[L] = e.in[q];
+      lp[L] = e.vpos[q], li[L] = e.in[q];
     }
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     double s = 0.0;
     if (e.K[r] != 0) {
-      double b[KMAX];
+      double a[KMAX], b[KMAX];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) b[k] = in[ix[r][k]];
+      for (int k = 0; k < KMAX; ++k) a[k] = v[vp[r][k]], b[k] = in[ix[r][k]];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) s += a[r][k] * b[k];
+      for (int k = 0; k < KMAX; ++k) s += a[k] * b[k];
     }
     out[r] = s;
   }
@@ -466,12 +457,12 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* val, const
 #pragma unroll
     for (int k = 0; k < LPF; ++k)
       if (k == L) {
-        if (lane < e.long_cnt[L]) s += lv[k] * in[li[k]];
+        if (lane < e.long_cnt[L]) s += v[lp[k]] * in[li[k]];
         t0 = lane + 64;
       }
     for (int t = t0; t < e.long_cnt[L]; t += 64) {
       const int q = e.long_off[L] + t;
-      s += val[q] * in[e.in[q]];
+      s += v[e.vpos[q]] * in[e.in[q]];
     }
     s = wave_sum(s);
     const int o = e.long_out[L];
@@ -562,25 +553,6 @@ __device__ __forceinline__ void load_vals(double* v, int base, const double* src
     }
   }
 }
-// gather the scaled values (scaling overlay in LDS) into the slab's ELL copies
-__device__ __forceinline__ void ell_park(const EllDev& e, const uint16_t* src, double* dst,
-                                         const double* v, int lane) {
-  constexpr int U = 8;
-  for (int t0 = 0; t0 < e.total; t0 += 64 * U) {
-    double x[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int t = t0 + 64 * u + lane;
-      x[u] = v[src[t < e.total ? t : 0]];  // padding -> S_ZERO
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int t = t0 + 64 * u + lane;
-      if (t < e.total) dst[t] = x[u];
-    }
-  }
-}
-
 template <int RN, int RM>
 __device__ __forceinline__ uint32_t ctype(const Inst<RN, RM>& S, int r) {
   return (S.ct >> (2 * r)) & 3u;
@@ -639,10 +611,10 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
   for (int j = lane; j < P.n; j += 64) v[P.slotSig[j]] = p.s.sigma;
   LDS_FENCE();
   for (int k = lane; k < P.nnzP; k += 64) {
-    const double val = sb.vP[P.posP[k]];
+    const double val = v[P.MV + k];
     v[P.slotP[k]] = (P.Pi[k] == P.Pcol[k]) ? val + p.s.sigma : val;
   }
-  for (int k = lane; k < P.nnzA; k += 64) v[P.slotA[k]] = sb.vA[P.posA[k]];
+  for (int k = lane; k < P.nnzA; k += 64) v[P.slotA[k]] = v[P.MV + P.nnzP + k];
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
@@ -680,18 +652,17 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   for (int r = 0; r < RM; ++r) yb[lane + 64 * r] = S.y[r];
   LDS_FENCE();
   double pr = 0.0, dr = 0.0;
-  const Slab& sbv = sb;
   T_END(T_RS0, t_r0);
   T_BEGIN(t_r1);
-  ell_mv<RM, ELL_KA>(P.eA, sbv.vA, xb, R.Ax, lane);  // padding terms are 0 * x
+  ell_mv<RM, ELL_KA>(P.eA, v, xb, R.Ax, lane);  // padding terms are 0 * x
   TSYNC(R.Ax[0]);
   T_END(T_RS1, t_r1);
   T_BEGIN(t_r2);
-  ell_mv<RN, ELL_KP>(P.eP, sbv.vP, xb, R.Px, lane);
+  ell_mv<RN, ELL_KP>(P.eP, v, xb, R.Px, lane);
   TSYNC(R.Px[0]);
   T_END(T_RS2, t_r2);
   T_BEGIN(t_r3);
-  ell_mv<RN, ELL_KAT>(P.eAt, sbv.vAt, yb, R.Aty, lane);
+  ell_mv<RN, ELL_KAT>(P.eAt, v, yb, R.Aty, lane);
   TSYNC(R.Aty[0]);
   T_END(T_RS3, t_r3);
   T_BEGIN(t_r4);
@@ -748,7 +719,7 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
   LDS_FENCE();
   // A' dy by the residual ELL (same term order as the CSC column traversal, loads batched)
   double aty[RN];
-  ell_mv<RN, ELL_KAT>(P.eAt, sb.vAt, yb, aty, lane);
+  ell_mv<RN, ELL_KAT>(P.eAt, v, yb, aty, lane);
   double mx = 0.0;
 #pragma unroll
   for (int r = 0; r < RN; ++r)
@@ -783,7 +754,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
   LDS_FENCE();
   // P dx and A dx by the residual ELLs (same term orders as the symmetric / CSR traversals)
   double pdx[RN];
-  ell_mv<RN, ELL_KP>(P.eP, sb.vP, xb, pdx, lane);
+  ell_mv<RN, ELL_KP>(P.eP, v, xb, pdx, lane);
   double mx = 0.0;
 #pragma unroll
   for (int r = 0; r < RN; ++r)
@@ -791,7 +762,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
   mx = wave_max(mx);
   if (!(mx < S.c * eps * nrm)) return false;
   double adx[RM];
-  ell_mv<RM, ELL_KA>(P.eA, sb.vA, xb, adx, lane);
+  ell_mv<RM, ELL_KA>(P.eA, v, xb, adx, lane);
   int bad = 0;
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
@@ -1053,11 +1024,27 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
     S.Dinv[r] = 1. / D[r];
     if (j < n) sb.D[j] = D[r];
   }
-  // park scaled P, A for residuals / refactorization (per-wave slab)
-  const uint16_t* ix = reinterpret_cast<const uint16_t*>(v) + P.SCI;
-  ell_park(P.eA, ix + P.sci_eA, sb.vA, v, lane);
-  ell_park(P.eAt, ix + P.sci_eAt, sb.vAt, v, lane);
-  ell_park(P.eP, ix + P.sci_eP, sb.vP, v, lane);
+  // the scaled values [P | A] stay resident in LDS (MV) for the residuals, certificates,
+  // (re)assembly and objective; the scaling overlay they come from is overwritten by the KKT image
+  LDS_FENCE();
+  {
+    const int cnt = P.nnzP + P.nnzA;
+    constexpr int U = 8;
+    for (int k0 = 0; k0 < cnt; k0 += 64 * U) {
+      double x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + 64 * u + lane;
+        x[u] = v[P.S_P + (k < cnt ? k : 0)];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + 64 * u + lane;
+        if (k < cnt) v[P.MV + k] = x[u];
+      }
+    }
+    if (lane == 0) v[P.MVZ] = 0.0;
+  }
   LDS_FENCE();
 }
 
@@ -1120,7 +1107,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       if (lane + 64 * r < n) xb[lane + 64 * r] = S.x[r];
     LDS_FENCE();
     double az[RM];
-    ell_mv<RM, ELL_KA>(P.eA, sb.vA, xb, az, lane);  // CSR row order
+    ell_mv<RM, ELL_KA>(P.eA, v, xb, az, lane);  // CSR row order
 #pragma unroll
     for (int r = 0; r < RM; ++r) S.z[r] = lane + 64 * r < m ? az[r] : 0.0;
     LDS_FENCE();
@@ -1180,9 +1167,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     // The forward solve accumulates into W, which starts at 0 except on the copy rows (first
     // block, empty reach: W_r = rhs_r, no solve task); the lanes' slots cover all of W
     uint32_t wcpi = wcp;  // re-derived every iteration (no hoisted per-slot lane masks)
-#ifndef LV_NOWCP
     asm volatile("" : "+v"(wcpi));
-#endif
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       xp[r] = S.x[r];
@@ -1256,12 +1241,12 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     if (can_check) chk_left = chk;
     const bool adapt = ar_int && --ar_left == 0;  // iter % ar_int == 0
     if (adapt) ar_left = ar_int;
-    // check-time code gets an opaque copy of the lane id: its per-lane addresses are recomputed at
-    // each check instead of being hoisted out of the ADMM loop into registers
+    // the larger buckets' check-time code gets an opaque copy of the lane id: its per-lane
+    // addresses are recomputed at each check instead of being hoisted out of the ADMM loop into
+    // registers (at RN = 4 the hoisted addresses spilled to scratch; at RN = 2 they fit in AGPRs
+    // and hoisting them measured faster)
     int clane = lane;
-#ifndef LV_NOCLANE
-    asm volatile("" : "+v"(clane));
-#endif
+    if constexpr (RN >= 4) asm volatile("" : "+v"(clane));
 #ifndef MPCQP_FIXED_WORK
     if (can_check || adapt) {
       T_BEGIN(t_rs);
@@ -1330,7 +1315,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     double part = 0.0;
     for (int k = lane; k < P.nnzP; k += 64) {
       const int i = P.Pi[k], j = P.Pcol[k];
-      const double pk = sb.vP[P.posP[k]];
+      const double pk = v[P.MV + k];
       part += (i == j) ? .5 * pk * xb[i] * xb[i] : pk * xb[i] * xb[j];
     }
 #pragma unroll
@@ -1399,13 +1384,10 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
     inst = __builtin_amdgcn_readfirstlane(inst);
     if (inst >= (unsigned int)p.B) break;
     if (p.skip && p.skip[inst]) continue;  // wave-uniform
-    // an opaque copy of the lane id per instance: per-lane address arithmetic cannot be hoisted
-    // out of the instance loop (held in registers for the whole kernel, it would cost the
-    // solve loop its occupancy)
+    // larger buckets: an opaque copy of the lane id per instance, so per-lane address arithmetic
+    // is not hoisted out of the instance loop (held in registers for the whole kernel it spills)
     int ilane = lane;
-#ifndef LV_NOILANE
-    asm volatile("" : "+v"(ilane));
-#endif
+    if constexpr (RN >= 4) asm volatile("" : "+v"(ilane));
     solve_instance<RN, RM, PAIRED>(p, (int)inst, v, scr, ilane);
     LDS_FENCE();
   }
@@ -1579,8 +1561,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
            o_eAi = push_blob(blob, pl.ellA.in), o_eTs = push_blob(blob, pl.ellAt.src),
            o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
            o_ePi = push_blob(blob, pl.ellP.in), o_sci = push_blob(blob, pl.sci_block),
-           o_pA = push_blob(blob, pl.posA), o_pP = push_blob(blob, pl.posP),
-           o_wc = push_blob(blob, pl.wcopy);
+           o_eAv = push_blob(blob, pl.ellA.vpos), o_eTv = push_blob(blob, pl.ellAt.vpos),
+           o_ePv = push_blob(blob, pl.ellP.vpos), o_wc = push_blob(blob, pl.wcopy);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
@@ -1592,7 +1574,6 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.nfac = pl.nfac, dp.ntail = pl.ntail, dp.nfwd = pl.nfwd, dp.nbwd = pl.nbwd;
     dp.Lcol = (const uint16_t*)(b + o_Lc);
     dp.slotP = (const uint16_t*)(b + o_sP), dp.slotA = (const uint16_t*)(b + o_sA);
-    dp.posA = (const uint16_t*)(b + o_pA), dp.posP = (const uint16_t*)(b + o_pP);
     dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
     dp.wsx = (const uint16_t*)(b + o_wx), dp.wsz = (const uint16_t*)(b + o_wz);
     dp.wcopy = (const uint32_t*)(b + o_wc);
@@ -1602,16 +1583,17 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.Pi = (const uint16_t*)(b + o_Pi), dp.Pcol = (const uint16_t*)(b + o_Pc);
     dp.Psp = (const uint16_t*)(b + o_Psp), dp.Psk = (const uint16_t*)(b + o_Psk);
     dp.Pso = (const uint16_t*)(b + o_Pso);
-    auto ell = [&](const Ell& e, size_t os, size_t oi, EllDev& d) {
+    auto ell = [&](const Ell& e, size_t os, size_t oi, size_t ov, EllDev& d) {
       d.src = (const uint16_t*)(b + os), d.in = (const uint16_t*)(b + oi), d.total = e.total;
+      d.vpos = (const uint16_t*)(b + ov);
       for (int r = 0; r < ELL_MAXR; ++r) d.K[r] = e.K[r], d.off[r] = e.off[r];
       d.nlong = e.nlong;
       for (int q = 0; q < ELL_MAXLONG; ++q)
         d.long_out[q] = e.long_out[q], d.long_off[q] = e.long_off[q], d.long_cnt[q] = e.long_cnt[q];
     };
-    ell(pl.ellA, o_eAs, o_eAi, dp.eA);
-    ell(pl.ellAt, o_eTs, o_eTi, dp.eAt);
-    ell(pl.ellP, o_ePs, o_ePi, dp.eP);
+    ell(pl.ellA, o_eAs, o_eAi, o_eAv, dp.eA);
+    ell(pl.ellAt, o_eTs, o_eTi, o_eTv, dp.eAt);
+    ell(pl.ellP, o_ePs, o_ePi, o_ePv, dp.eP);
     dp.inst_doubles = (pl.LDS_N + 1) & ~1;
     dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
     dp.nnzL = pl.nnzL;
@@ -1622,6 +1604,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.sci_n16 = (int)(pl.sci_block.size() / 8);
     dp.sci_eP = pl.sci_eP, dp.sci_eAt = pl.sci_eAt, dp.sci_eA = pl.sci_eA;
     dp.sci_ra = pl.sci_ra, dp.sci_ca = pl.sci_ca;
+    dp.MV = pl.MV, dp.MVZ = pl.MVZ;
 
     // occupancy (LDS image and VGPRs) -> persistent grid
     int dev = 0, ncu = 0;
@@ -1657,9 +1640,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->Ecls, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
-            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid *
-                                       slab_doubles(pl.n, pl.m, pl.ellA.total, pl.ellAt.total,
-                                                    pl.ellP.total)) == hipSuccess &&
+            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid * slab_doubles(pl.n, pl.m)) ==
+                hipSuccess &&
             hipMalloc(&h->counter, 64) == hipSuccess;
   if (!ok) return cleanup_fail(MPCQP_E_HIP, "hipMalloc(batch buffers)");
   if (hipMemset(h->has_state, 0, sizeof(int32_t) * Bz) != hipSuccess)

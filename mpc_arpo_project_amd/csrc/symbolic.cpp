@@ -1210,6 +1210,19 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
       return false;
     }
   }
+  // ---- resident scaled values (Plan::MV) behind the image; the ELL terms' LDS value slots
+  pl.MV = (pl.LDS_N + 1) & ~1;
+  pl.MVZ = pl.MV + pl.nnzP + pl.nnzA;
+  pl.LDS_N = (pl.MVZ + 2) & ~1;
+  if (pl.LDS_N * 8 > (int)META_TGT_MASK || pl.LDS_N >= 65535) {
+    pl.error = "LDS image too large for the resident matrix values";
+    return false;
+  }
+  for (Ell* e : {&pl.ellA, &pl.ellAt, &pl.ellP}) {
+    e->vpos.resize(e->src.size());
+    for (size_t t = 0; t < e->src.size(); ++t)
+      e->vpos[t] = (uint16_t)(e->src[t] == 0xffff ? pl.MVZ : pl.MV + (e->src[t] - pl.S_P));
+  }
   return true;
 }
 

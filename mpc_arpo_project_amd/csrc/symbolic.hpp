@@ -72,6 +72,10 @@ struct Ell {
   int nlong = 0;
   int long_out[ELL_MAXLONG] = {}, long_off[ELL_MAXLONG] = {}, long_cnt[ELL_MAXLONG] = {};
   std::vector<uint16_t> src, in;
+  // LDS slot (doubles) of each term's scaled value in the resident value region MV (CSC order,
+  // Plan::MV); padding terms point at the zero slot MVZ.  The residual mat-vecs read the values
+  // from LDS through it (the indices are shared by every instance: L1/L2 hits)
+  std::vector<uint16_t> vpos;
 };
 
 // Register-slot bucket of the engine kernel: RN >= ceil(n / 64) slots for n-vectors, RM >= ceil(m /
@@ -118,6 +122,10 @@ struct Plan {
   // lists of P, A', A and the (row, column) of every P and A entry, copied in once per solve so
   // the Ruiz passes read indices from LDS; offsets relative to SCI
   int SCI = 0, S_ZERO = 0;  // S_ZERO: a zero double (in doubles) for the ELL padding
+  // resident scaled matrix values [P (upper CSC) | A (CSC)] behind everything else of the image:
+  // written at the end of the Ruiz scaling, read by the residual mat-vecs, the infeasibility
+  // certificates, every (re)assembly of the KKT values and the objective; MVZ holds a zero
+  int MV = 0, MVZ = 0;
   int sci_eP = 0, sci_eAt = 0, sci_eA = 0;
   // the Ruiz rescale's operand slots of the value overlay [P | A] (CSC orders): row scaling slot
   // (S_DT + i for P, S_ET + i for A) and column scaling slot (S_DT + j)
