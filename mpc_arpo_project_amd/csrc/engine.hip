@@ -43,6 +43,7 @@ namespace {
 // ------------------------------------------------------------------------------------- device
 struct EllDev {
   const uint16_t *src, *in, *vpos;
+  const uint32_t* pk;  // lane-major packed (vpos, in) terms of the used slots (symbolic.hpp Ell::pk)
   int K[ELL_MAXR], off[ELL_MAXR];
   int total, nlong;
   int long_out[ELL_MAXLONG], long_off[ELL_MAXLONG], long_cnt[ELL_MAXLONG];
@@ -415,15 +416,16 @@ __device__ __forceinline__ Slab slab_of(const DevPlan& P, double* scr) {
 template <int R, int KMAX>
 __device__ __forceinline__ void ell_mv(const EllDev& e, const double* v, const double* in,
                                        double (&out)[R], int lane) {
-  uint32_t vp[R][KMAX], ix[R][KMAX];
+  static_assert(KMAX % 4 == 0, "lane-major term rows are loaded 16 bytes at a time");
+  uint32_t tk[R][KMAX];  // packed (value slot, input index) of this lane's terms
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (e.K[r] == 0) continue;  // slot beyond the instance (wave-uniform)
+    const uint4* row = reinterpret_cast<const uint4*>(e.pk + (size_t)(r * 64 + lane) * KMAX);
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const int t = e.off[r] + 64 * k + lane;
-      vp[r][k] = e.vpos[t];
-      ix[r][k] = e.in[t];
+    for (int q = 0; q < KMAX / 4; ++q) {
+      const uint4 w = row[q];
+      tk[r][4 * q] = w.x, tk[r][4 * q + 1] = w.y, tk[r][4 * q + 2] = w.z, tk[r][4 * q + 3] = w.w;
     }
   }
   // outputs with more than KMAX terms: the first 64 terms' loads of the first LPF of them go out
@@ -444,7 +446,7 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* v, const d
     if (e.K[r] != 0) {
       double a[KMAX], b[KMAX];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) a[k] = v[vp[r][k]], b[k] = in[ix[r][k]];
+      for (int k = 0; k < KMAX; ++k) a[k] = v[tk[r][k] & 0xffffu], b[k] = in[tk[r][k] >> 16];
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) s += a[k] * b[k];
     }
@@ -1562,7 +1564,9 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
            o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
            o_ePi = push_blob(blob, pl.ellP.in), o_sci = push_blob(blob, pl.sci_block),
            o_eAv = push_blob(blob, pl.ellA.vpos), o_eTv = push_blob(blob, pl.ellAt.vpos),
-           o_ePv = push_blob(blob, pl.ellP.vpos), o_wc = push_blob(blob, pl.wcopy);
+           o_ePv = push_blob(blob, pl.ellP.vpos), o_eAk = push_blob(blob, pl.ellA.pk),
+           o_eTk = push_blob(blob, pl.ellAt.pk), o_ePk = push_blob(blob, pl.ellP.pk),
+           o_wc = push_blob(blob, pl.wcopy);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
@@ -1583,17 +1587,17 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.Pi = (const uint16_t*)(b + o_Pi), dp.Pcol = (const uint16_t*)(b + o_Pc);
     dp.Psp = (const uint16_t*)(b + o_Psp), dp.Psk = (const uint16_t*)(b + o_Psk);
     dp.Pso = (const uint16_t*)(b + o_Pso);
-    auto ell = [&](const Ell& e, size_t os, size_t oi, size_t ov, EllDev& d) {
+    auto ell = [&](const Ell& e, size_t os, size_t oi, size_t ov, size_t ok, EllDev& d) {
       d.src = (const uint16_t*)(b + os), d.in = (const uint16_t*)(b + oi), d.total = e.total;
-      d.vpos = (const uint16_t*)(b + ov);
+      d.vpos = (const uint16_t*)(b + ov), d.pk = (const uint32_t*)(b + ok);
       for (int r = 0; r < ELL_MAXR; ++r) d.K[r] = e.K[r], d.off[r] = e.off[r];
       d.nlong = e.nlong;
       for (int q = 0; q < ELL_MAXLONG; ++q)
         d.long_out[q] = e.long_out[q], d.long_off[q] = e.long_off[q], d.long_cnt[q] = e.long_cnt[q];
     };
-    ell(pl.ellA, o_eAs, o_eAi, o_eAv, dp.eA);
-    ell(pl.ellAt, o_eTs, o_eTi, o_eTv, dp.eAt);
-    ell(pl.ellP, o_ePs, o_ePi, o_ePv, dp.eP);
+    ell(pl.ellA, o_eAs, o_eAi, o_eAv, o_eAk, dp.eA);
+    ell(pl.ellAt, o_eTs, o_eTi, o_eTv, o_eTk, dp.eAt);
+    ell(pl.ellP, o_ePs, o_ePi, o_ePv, o_ePk, dp.eP);
     dp.inst_doubles = (pl.LDS_N + 1) & ~1;
     dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
     dp.nnzL = pl.nnzL;

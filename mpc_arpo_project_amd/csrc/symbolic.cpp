@@ -1222,6 +1222,13 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     e->vpos.resize(e->src.size());
     for (size_t t = 0; t < e->src.size(); ++t)
       e->vpos[t] = (uint16_t)(e->src[t] == 0xffff ? pl.MVZ : pl.MV + (e->src[t] - pl.S_P));
+    e->pk.assign((size_t)e->R * 64 * e->kmax, 0u);
+    for (int r = 0; r < e->R; ++r)
+      for (int l = 0; l < 64; ++l)
+        for (int k = 0; k < e->kmax; ++k) {
+          const int t = e->off[r] + 64 * k + l;
+          e->pk[((size_t)r * 64 + l) * e->kmax + k] = (uint32_t)e->vpos[t] | ((uint32_t)e->in[t] << 16);
+        }
   }
   return true;
 }

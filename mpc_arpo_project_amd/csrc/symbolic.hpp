@@ -76,6 +76,9 @@ struct Ell {
   // Plan::MV); padding terms point at the zero slot MVZ.  The residual mat-vecs read the values
   // from LDS through it (the indices are shared by every instance: L1/L2 hits)
   std::vector<uint16_t> vpos;
+  // the same terms lane-major for the kernel's loads: for used slot r, lane l, term k,
+  // pk[(r * 64 + l) * kmax + k] = vpos | in << 16 (one 16-byte load covers four terms)
+  std::vector<uint32_t> pk;
 };
 
 // Register-slot bucket of the engine kernel: RN >= ceil(n / 64) slots for n-vectors, RM >= ceil(m /
