@@ -42,7 +42,7 @@ namespace {
 
 // ------------------------------------------------------------------------------------- device
 struct EllDev {
-  const uint16_t *src, *in, *vpos;
+  const uint16_t *src, *in, *vpos, *sk;
   const uint32_t* pk;  // lane-major packed (vpos, in) terms of the used slots (symbolic.hpp Ell::pk)
   int K[ELL_MAXR], off[ELL_MAXR];
   int total, nlong;
@@ -59,11 +59,11 @@ struct DevPlan {
   int n, m, nk, nnzP, nnzA, nnzL;
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
   int NKS;  // 64-lane slots of the padded 1/D, W and C regions (symbolic.hpp NKP / 64 = RN + RM)
-  // scaling index overlay (symbolic.hpp): 16-byte chunks copied to LDS at u16 offset SCI
   const uint32_t* wcopy;  // per lane: register slots holding copy rows (symbolic.hpp Plan::wcopy)
-  const uint4* sci_src;
-  int SCI, S_ZERO, sci_n16, sci_eP, sci_eAt, sci_eA, sci_ra, sci_ca;
+  int S_ZERO;
   int MV, MVZ;  // resident scaled values [P | A] (CSC orders) and their zero slot
+  const uint16_t *sra, *sca;  // lane-major row / column scaling slots (symbolic.hpp Plan::sra)
+  int SJ;
 };
 
 struct KParams {
@@ -473,25 +473,41 @@ __device__ __forceinline__ void ell_mv(const EllDev& e, const double* v, const d
       if (o == lane + 64 * r) out[r] = s;
   }
 }
-// out[r] = max_k |v[src]| over the ELL terms of slot r (the infinity norms of Ruiz scaling; max is
-// order-free, so any traversal equals OSQP's).  All index loads are issued before the LDS reads.
+// The Ruiz passes' index lists, loaded once per solve into registers (lane-major, 8 bytes = four
+// u16 slots per load; shared by every instance: L1/L2 hits): the passes then read only values.
 template <int R, int KMAX>
-__device__ __forceinline__ void ell_absmax(const EllDev& e, const uint16_t* src, const double* v,
-                                           double (&out)[R], int lane) {
-  uint32_t ix[R][KMAX];
+struct EllIdx {
+  uint32_t w[R][KMAX / 2];  // two u16 overlay slots per register
+};
+template <int R, int KMAX>
+__device__ __forceinline__ void load_idx(const EllDev& e, EllIdx<R, KMAX>& ix, int lane) {
+  static_assert(KMAX % 4 == 0, "index rows are loaded 8 bytes at a time");
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (e.K[r] == 0) continue;
+    const uint2* row = reinterpret_cast<const uint2*>(e.sk + (size_t)(r * 64 + lane) * KMAX);
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) ix[r][k] = src[e.off[r] + 64 * k + lane];
+    for (int q = 0; q < KMAX / 4; ++q) {
+      const uint2 w = row[q];
+      ix.w[r][2 * q] = w.x, ix.w[r][2 * q + 1] = w.y;
+    }
   }
+}
+// out[r] = max_k |v[slot]| over the ELL terms of slot r, indices from registers (max is
+// order-free, so any traversal equals OSQP's); long outputs read their slots from global memory
+template <int R, int KMAX>
+__device__ __forceinline__ void ell_absmax_r(const EllDev& e, const EllIdx<R, KMAX>& ix,
+                                             const double* v, double (&out)[R], int lane) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     double mx = 0.0;
     if (e.K[r] != 0) {
       double b[KMAX];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) b[k] = v[ix[r][k]];  // padding -> S_ZERO
+      for (int k = 0; k < KMAX; ++k) {
+        const uint32_t w = ix.w[r][k / 2];
+        b[k] = v[(k & 1) ? (w >> 16) : (w & 0xffffu)];  // padding -> S_ZERO
+      }
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) mx = dmaxd(fabs(b[k]), mx);
     }
@@ -499,7 +515,7 @@ __device__ __forceinline__ void ell_absmax(const EllDev& e, const uint16_t* src,
   }
   for (int L = 0; L < e.nlong; ++L) {
     double mx = 0.0;
-    for (int t = lane; t < e.long_cnt[L]; t += 64) mx = dmaxd(fabs(v[src[e.long_off[L] + t]]), mx);
+    for (int t = lane; t < e.long_cnt[L]; t += 64) mx = dmaxd(fabs(v[e.src[e.long_off[L] + t]]), mx);
     mx = wave_max(mx);
     const int o = e.long_out[L];
 #pragma unroll
@@ -511,28 +527,29 @@ __device__ __forceinline__ void ell_absmax(const EllDev& e, const uint16_t* src,
 //   v[S_P + k] = ((v[S_P + k] * f) * v[ra[k]]) * v[ca[k]],  f = cp for P's values, 1 for A's
 // -- scaling.c's mat_premult_diag / mat_postmult_diag, with the previous pass's cost factor c
 // (mat_mult_scalar on P) deferred into this pass: the same multiplications in the same order, and
-// x * 1.0 is exact.  All index reads of a batch, then all value reads, then the stores.
-__device__ __forceinline__ void scale_pa(double* v, int S_P, int nnzP, int cnt, const uint16_t* ra,
-                                         const uint16_t* ca, double cp, int lane) {
-  constexpr int U = 16;
-  for (int k0 = 0; k0 < cnt; k0 += 64 * U) {
-    uint32_t a[U], b[U];
+// x * 1.0 is exact.  The row / column scaling slots come from registers (JW pairs of u16 per
+// lane: value k = 64 j + lane, j < 2 JW).
+template <int JW>
+__device__ __forceinline__ void scale_pa_r(double* v, int S_P, int nnzP, int cnt,
+                                           const uint32_t (&ra)[JW], const uint32_t (&ca)[JW],
+                                           double cp, int lane) {
+  constexpr int U = 8;  // values in flight per lane: all value reads of a batch, then its stores
+  static_assert((2 * JW) % U == 0, "batches of U values");
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = k0 + 64 * u + lane, kc = k < cnt ? k : 0;
-      a[u] = ra[kc];
-      b[u] = ca[kc];
-    }
+  for (int j0 = 0; j0 < 2 * JW; j0 += U) {
+    if (64 * j0 >= cnt) break;  // wave-uniform
     double x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k = k0 + 64 * u + lane, kc = k < cnt ? k : 0;
+      const int j = j0 + u, k = 64 * j + lane, kc = k < cnt ? k : 0;
       const double f = k < nnzP ? cp : 1.0;
-      x[u] = ((v[S_P + kc] * f) * v[a[u]]) * v[b[u]];
+      const uint32_t a = (j & 1) ? (ra[j / 2] >> 16) : (ra[j / 2] & 0xffffu);
+      const uint32_t b = (j & 1) ? (ca[j / 2] >> 16) : (ca[j / 2] & 0xffffu);
+      x[u] = ((v[S_P + kc] * f) * v[a]) * v[b];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k = k0 + 64 * u + lane;
+      const int k = 64 * (j0 + u) + lane;
       if (k < cnt) v[S_P + k] = x[u];
     }
   }
@@ -892,25 +909,28 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
   const double* Ax_in = p.Ax + (size_t)inst * P.nnzA;
   const double* l_in = p.l + (size_t)inst * m;
   const double* u_in = p.u + (size_t)inst * m;
-  {  // scaling index overlay -> LDS (read by every pass below and by scale_finish)
-    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(v) + P.SCI);
-    constexpr int U = 8;
-    for (int k0 = 0; k0 < P.sci_n16; k0 += 64 * U) {
-      uint4 t[U];
+  // the passes' index lists in registers (shared structure arrays, loaded once per solve)
+  EllIdx<RN, ELL_KP> iP;
+  EllIdx<RN, ELL_KAT> iAt;
+  EllIdx<RM, ELL_KA> iA;
+  load_idx(P.eP, iP, lane);
+  load_idx(P.eAt, iAt, lane);
+  load_idx(P.eA, iA, lane);
+  constexpr int JW = 4 * RN;  // u16 pairs of row / column slots per lane (Plan::SJ <= 2 JW)
+  uint32_t ra[JW], ca[JW];
+  {
+    const uint2* rr = reinterpret_cast<const uint2*>(P.sra + (size_t)lane * P.SJ);
+    const uint2* cc = reinterpret_cast<const uint2*>(P.sca + (size_t)lane * P.SJ);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = k0 + 64 * u + lane;
-        t[u] = P.sci_src[k < P.sci_n16 ? k : 0];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = k0 + 64 * u + lane;
-        if (k < P.sci_n16) d[k] = t[u];
+    for (int q = 0; q < JW / 2; ++q) {
+      ra[2 * q] = ra[2 * q + 1] = ca[2 * q] = ca[2 * q + 1] = 0u;
+      if (4 * q < P.SJ) {  // wave-uniform
+        const uint2 a = rr[q], c = cc[q];
+        ra[2 * q] = a.x, ra[2 * q + 1] = a.y, ca[2 * q] = c.x, ca[2 * q + 1] = c.y;
       }
     }
   }
   if (lane == 0) v[P.S_ZERO] = 0.0;
-  const uint16_t* ix = reinterpret_cast<const uint16_t*>(v) + P.SCI;
   load_vals(v, P.S_P, p.Px, P.nnzP, lane);
   load_vals(v, P.S_A, Ax_in, P.nnzA, lane);
 #pragma unroll
@@ -937,13 +957,13 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
     // monotonic (c > 0)
     double dp[RN], da[RN], er[RM], dt[RN], et[RM];
     if (it == 0) {
-      ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dp, lane);
+      ell_absmax_r(P.eP, iP, v, dp, lane);
     } else {
 #pragma unroll
       for (int r = 0; r < RN; ++r) dp[r] = cprev * dpc[r];
     }
-    ell_absmax<RN, ELL_KAT>(P.eAt, ix + P.sci_eAt, v, da, lane);
-    ell_absmax<RM, ELL_KA>(P.eA, ix + P.sci_eA, v, er, lane);
+    ell_absmax_r(P.eAt, iAt, v, da, lane);
+    ell_absmax_r(P.eA, iA, v, er, lane);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const int j = lane + 64 * r;
@@ -959,7 +979,7 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
       if (i < m) v[P.S_ET + i] = et[r];
     }
     LDS_FENCE();
-    scale_pa(v, P.S_P, P.nnzP, P.nnzP + P.nnzA, ix + P.sci_ra, ix + P.sci_ca, cprev, lane);
+    scale_pa_r(v, P.S_P, P.nnzP, P.nnzP + P.nnzA, ra, ca, cprev, lane);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       S.q[r] = dt[r] * S.q[r];
@@ -969,7 +989,7 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
     for (int r = 0; r < RM; ++r) E[r] = E[r] * et[r];
     LDS_FENCE();
     // cost normalization: mean of P's column norms, |q|_inf
-    ell_absmax<RN, ELL_KP>(P.eP, ix + P.sci_eP, v, dpc, lane);
+    ell_absmax_r(P.eP, iP, v, dpc, lane);
     double csum = 0.0, qmax = 0.0;
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
@@ -1562,11 +1582,13 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
            o_Pso = push_blob(blob, pl.Pso), o_eAs = push_blob(blob, pl.ellA.src),
            o_eAi = push_blob(blob, pl.ellA.in), o_eTs = push_blob(blob, pl.ellAt.src),
            o_eTi = push_blob(blob, pl.ellAt.in), o_ePs = push_blob(blob, pl.ellP.src),
-           o_ePi = push_blob(blob, pl.ellP.in), o_sci = push_blob(blob, pl.sci_block),
+           o_ePi = push_blob(blob, pl.ellP.in),
            o_eAv = push_blob(blob, pl.ellA.vpos), o_eTv = push_blob(blob, pl.ellAt.vpos),
            o_ePv = push_blob(blob, pl.ellP.vpos), o_eAk = push_blob(blob, pl.ellA.pk),
            o_eTk = push_blob(blob, pl.ellAt.pk), o_ePk = push_blob(blob, pl.ellP.pk),
-           o_wc = push_blob(blob, pl.wcopy);
+           o_eAq = push_blob(blob, pl.ellA.sk), o_eTq = push_blob(blob, pl.ellAt.sk),
+           o_ePq = push_blob(blob, pl.ellP.sk), o_sra = push_blob(blob, pl.sra),
+           o_sca = push_blob(blob, pl.sca), o_wc = push_blob(blob, pl.wcopy);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
@@ -1587,28 +1609,30 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.Pi = (const uint16_t*)(b + o_Pi), dp.Pcol = (const uint16_t*)(b + o_Pc);
     dp.Psp = (const uint16_t*)(b + o_Psp), dp.Psk = (const uint16_t*)(b + o_Psk);
     dp.Pso = (const uint16_t*)(b + o_Pso);
-    auto ell = [&](const Ell& e, size_t os, size_t oi, size_t ov, size_t ok, EllDev& d) {
+    auto ell = [&](const Ell& e, size_t os, size_t oi, size_t ov, size_t ok, size_t oq,
+                   EllDev& d) {
       d.src = (const uint16_t*)(b + os), d.in = (const uint16_t*)(b + oi), d.total = e.total;
       d.vpos = (const uint16_t*)(b + ov), d.pk = (const uint32_t*)(b + ok);
+      d.sk = (const uint16_t*)(b + oq);
       for (int r = 0; r < ELL_MAXR; ++r) d.K[r] = e.K[r], d.off[r] = e.off[r];
       d.nlong = e.nlong;
       for (int q = 0; q < ELL_MAXLONG; ++q)
         d.long_out[q] = e.long_out[q], d.long_off[q] = e.long_off[q], d.long_cnt[q] = e.long_cnt[q];
     };
-    ell(pl.ellA, o_eAs, o_eAi, o_eAv, o_eAk, dp.eA);
-    ell(pl.ellAt, o_eTs, o_eTi, o_eTv, o_eTk, dp.eAt);
-    ell(pl.ellP, o_ePs, o_ePi, o_ePv, o_ePk, dp.eP);
+    ell(pl.ellA, o_eAs, o_eAi, o_eAv, o_eAk, o_eAq, dp.eA);
+    ell(pl.ellAt, o_eTs, o_eTi, o_eTv, o_eTk, o_eTq, dp.eAt);
+    ell(pl.ellP, o_ePs, o_ePi, o_ePv, o_ePk, o_ePq, dp.eP);
     dp.inst_doubles = (pl.LDS_N + 1) & ~1;
     dp.n = pl.n, dp.m = pl.m, dp.nk = pl.nk, dp.nnzP = pl.nnzP, dp.nnzA = pl.nnzA;
     dp.nnzL = pl.nnzL;
     dp.LX = pl.LX, dp.DINV = pl.DINV, dp.W = pl.W, dp.CACC = pl.CACC, dp.ZERO = pl.ZERO;
     dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N, dp.NKS = pl.NKP / 64;
     dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
-    dp.sci_src = (const uint4*)(b + o_sci), dp.SCI = pl.SCI, dp.S_ZERO = pl.S_ZERO;
-    dp.sci_n16 = (int)(pl.sci_block.size() / 8);
-    dp.sci_eP = pl.sci_eP, dp.sci_eAt = pl.sci_eAt, dp.sci_eA = pl.sci_eA;
-    dp.sci_ra = pl.sci_ra, dp.sci_ca = pl.sci_ca;
+    dp.S_ZERO = pl.S_ZERO;
     dp.MV = pl.MV, dp.MVZ = pl.MVZ;
+    dp.sra = (const uint16_t*)(b + o_sra), dp.sca = (const uint16_t*)(b + o_sca), dp.SJ = pl.SJ;
+    if (pl.SJ > 8 * pl.RN)  // the kernel holds 8 RN row / column slots per lane (scale_problem)
+      return cleanup_fail(MPCQP_E_UNSUPPORTED, "too many matrix values for the scaling registers");
 
     // occupancy (LDS image and VGPRs) -> persistent grid
     int dev = 0, ncu = 0;

@@ -1197,18 +1197,22 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
       ra.push_back((uint16_t)(pl.S_ET + pl.Ai[k])), ca.push_back((uint16_t)(pl.S_DT + pl.Acol[k]));
     put(ra, (int)ra.size(), pl.sci_ra);
     put(ca, (int)ca.size(), pl.sci_ca);
+    const int cnt = (int)ra.size();
+    pl.SJ = ((cnt + 63) / 64 + 3) / 4 * 4;
+    pl.sra.assign((size_t)64 * pl.SJ, 0);
+    pl.sca.assign((size_t)64 * pl.SJ, 0);
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < pl.SJ; ++j) {
+        const int k = 64 * j + l;
+        pl.sra[(size_t)l * pl.SJ + j] = k < cnt ? ra[k] : 0;
+        pl.sca[(size_t)l * pl.SJ + j] = k < cnt ? ca[k] : 0;
+      }
     while (b.size() % 8) b.push_back(0);
     // ELL padding reads a zero double kept behind the value overlay (no conditional LDS reads)
     pl.S_ZERO = pl.S_ET + m;
     for (int k = 0; k < pl.sci_ra; ++k)
       if (b[k] == 0xffff) b[k] = (uint16_t)pl.S_ZERO;
-    pl.SCI = ((pl.S_ZERO + 1) * 4 + 7) & ~7;  // u16 units, 16-byte aligned
-    const int end = pl.SCI + (int)b.size();
-    if (end > pl.LDS_N * 4) pl.LDS_N = (((end + 3) / 4) + 1) & ~1;
-    if (pl.LDS_N * 8 > (int)META_TGT_MASK || pl.LDS_N >= 65535) {
-      pl.error = "LDS image too large for the scaling index overlay";
-      return false;
-    }
+    if (pl.S_ZERO + 1 > pl.LDS_N) pl.LDS_N = (pl.S_ZERO + 2) & ~1;
   }
   // ---- resident scaled values (Plan::MV) behind the image; the ELL terms' LDS value slots
   pl.MV = (pl.LDS_N + 1) & ~1;
@@ -1222,6 +1226,13 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     e->vpos.resize(e->src.size());
     for (size_t t = 0; t < e->src.size(); ++t)
       e->vpos[t] = (uint16_t)(e->src[t] == 0xffff ? pl.MVZ : pl.MV + (e->src[t] - pl.S_P));
+    e->sk.assign((size_t)e->R * 64 * e->kmax, (uint16_t)pl.S_ZERO);
+    for (int r = 0; r < e->R; ++r)
+      for (int l = 0; l < 64; ++l)
+        for (int k = 0; k < e->kmax; ++k) {
+          const uint16_t x = e->src[e->off[r] + 64 * k + l];
+          e->sk[((size_t)r * 64 + l) * e->kmax + k] = x == 0xffff ? (uint16_t)pl.S_ZERO : x;
+        }
     e->pk.assign((size_t)e->R * 64 * e->kmax, 0u);
     for (int r = 0; r < e->R; ++r)
       for (int l = 0; l < 64; ++l)

@@ -79,6 +79,9 @@ struct Ell {
   // the same terms lane-major for the kernel's loads: for used slot r, lane l, term k,
   // pk[(r * 64 + l) * kmax + k] = vpos | in << 16 (one 16-byte load covers four terms)
   std::vector<uint32_t> pk;
+  // the terms' scaling-overlay slots (src, padding -> S_ZERO) lane-major like pk, u16: the Ruiz
+  // passes keep them in registers for the whole scaling
+  std::vector<uint16_t> sk;
 };
 
 // Register-slot bucket of the engine kernel: RN >= ceil(n / 64) slots for n-vectors, RM >= ceil(m /
@@ -133,6 +136,10 @@ struct Plan {
   // the Ruiz rescale's operand slots of the value overlay [P | A] (CSC orders): row scaling slot
   // (S_DT + i for P, S_ET + i for A) and column scaling slot (S_DT + j)
   int sci_ra = 0, sci_ca = 0;
+  // the same row / column scaling slots lane-major: value k = 64 j + l of [P | A] at [l][j],
+  // j < SJ (a multiple of 4; padding -> S_ZERO), held in registers by the Ruiz passes
+  int SJ = 0;
+  std::vector<uint16_t> sra, sca;
   std::vector<uint16_t> sci_block;  // padded to a multiple of 8 entries
   // KKT assembly: LDS slot of each P entry (diagonal -> D slot), A entry, rho diagonal,
   // sigma diagonal (D slot of x_j)
