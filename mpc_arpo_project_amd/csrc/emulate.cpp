@@ -123,9 +123,10 @@ bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, doubl
   };
   run_solve_table(pl.fwd, pl.nfwd, pl.paired, v);
   bool intact = dinv_intact();
-  for (int k = 0; k < pl.NKP; ++k) {
-    v[pl.CACC + k] = v[pl.W + k] * v[pl.DINV + k];
-    v[pl.W + k] = 0.0;
+  for (int k = 0; k < pl.NKP; ++k) {  // backward copy rows keep (1/D) W in W (Plan::bcopy)
+    const double c = v[pl.W + k] * v[pl.DINV + k];
+    v[pl.CACC + k] = c;
+    v[pl.W + k] = (pl.bcopy[k % 64] >> (k / 64)) & 1u ? c : 0.0;
   }
   run_solve_table(pl.bwd, pl.nbwd, pl.paired, v);
   intact = intact && dinv_intact();

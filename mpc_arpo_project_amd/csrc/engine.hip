@@ -59,7 +59,8 @@ struct DevPlan {
   int n, m, nk, nnzP, nnzA, nnzL;
   int LX, DINV, W, CACC, ZERO, ONE, MONE, LDS_N, S_P, S_A, S_DT, S_ET;
   int NKS;  // 64-lane slots of the padded 1/D, W and C regions (symbolic.hpp NKP / 64 = RN + RM)
-  const uint32_t* wcopy;  // per lane: register slots holding copy rows (symbolic.hpp Plan::wcopy)
+  const uint32_t* wcopy;  // per lane: register slots whose W starts at the rhs (symbolic.hpp Plan::wcopy)
+  const uint32_t* bcopy;  // per lane: diagonal-pass slots whose W starts at (1/D) W (Plan::bcopy)
   int S_ZERO;
   int MV, MVZ;  // resident scaled values [P | A] (CSC orders) and their zero slot
   const uint16_t *sra, *sca;  // lane-major row / column scaling slots (symbolic.hpp Plan::sra)
@@ -207,6 +208,21 @@ __device__ __forceinline__ void load_solve(Rsrc rs, int soff, uint32_t lane, Sol
       __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + 4 * SOLVE_TERM_WORDS, soff, 0);
   r.t0 = tg[0], r.t1 = tg[1], r.t2 = tg[2], r.t3 = tg[3];
 }
+#ifdef EXP_AGPR
+__device__ __forceinline__ uint32_t agpr_rt(uint32_t x) {
+  uint32_t a, v;
+  asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(a) : "v"(x));
+  asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(a));
+  return v;
+}
+__device__ __forceinline__ void agpr_reload(SolveRec& r) {
+#pragma unroll
+  for (int c = 0; c < SOLVE_MAXC; ++c) r.a[c] = agpr_rt(r.a[c]), r.b[c] = agpr_rt(r.b[c]);
+  r.t0 = agpr_rt(r.t0), r.t2 = agpr_rt(r.t2), r.t3 = agpr_rt(r.t3);
+}
+template <typename R>
+__device__ __forceinline__ void agpr_reload(R&) {}
+#endif
 // one lane's records of a factorization step: meta word + FAC_MAXC (a, b, c, -) address quads
 struct FacRec {
   uint32_t mt;
@@ -324,12 +340,24 @@ __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops
 // The rotation is unrolled 12 steps deep: LLVM's waitcnt insertion merges states pessimistically
 // at a loop header (the first step after it would wait for all three sets), so the header is
 // reached at most once per ~12 steps.
+#if defined(EXP_NOREC)
+#define MPCQP_STEP(X)                                       \
+  ops.step(p.X, s);                                         \
+  if (++s >= n) break;
+#elif defined(EXP_AGPR)
+// ablation: the records of step s + 2 re-read from AGPR copies (19 v_accvgpr_read), no VMEM
+#define MPCQP_STEP(X)                                       \
+  ops.step(p.X, s);                                         \
+  if (++s >= n) break;                                      \
+  agpr_reload(p.X);
+#else
 #define MPCQP_STEP(X)                                       \
   ops.step(p.X, s);                                         \
   if (++s >= n) break;                                      \
   __builtin_amdgcn_sched_barrier(0);                        \
   Ops::load(rs, step_off<Ops>(n, s + 2), lane, p.X);        \
   __builtin_amdgcn_sched_barrier(0);
+#endif
 template <typename Ops>
 __device__ __forceinline__ void run_body(Rsrc rs, int n, uint32_t lane, const Ops& ops,
                                          Pipe<Ops>& p) {
@@ -1153,7 +1181,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   // of NKP = 64 (RN + RM) doubles (symbolic.cpp relocate), a compile-time constant: the stores'
   // immediate offset, so no second address register per slot
   constexpr int coff = 64 * (RN + RM);
-  const uint32_t wcp = P.wcopy[lane];
+  const uint32_t wcp = P.wcopy[lane], bcp = P.bcopy[lane];
   // loop constants held in VGPRs (an opaque copy: otherwise they are re-read from the kernel
   // arguments inside the loop, with an lgkmcnt(0) wait that also drains the LDS queue)
   double sigma = p.s.sigma, alpha = p.s.alpha, alpha_c = 1.0 - p.s.alpha;
@@ -1213,6 +1241,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     T_BEGIN(t_v1);
     prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
     {
+      // C = (1/D) W; W restarts at 0, or at C where the row's identity term is folded into it
+      // (Plan::bcopy: the backward task has no MONE term)
+      uint32_t bcpi = bcp;  // re-derived every iteration (no hoisted per-slot lane masks)
+      asm volatile("" : "+v"(bcpi));
       double wv[RN + RM], dv[RN + RM];
 #pragma unroll
       for (int r = 0; r < RN + RM; ++r) {
@@ -1221,8 +1253,9 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       }
 #pragma unroll
       for (int r = 0; r < RN + RM; ++r) {
-        v[P.CACC + lane + 64 * r] = wv[r] * dv[r];
-        v[P.W + lane + 64 * r] = 0.0;
+        const double c = wv[r] * dv[r];
+        v[P.CACC + lane + 64 * r] = c;
+        v[P.W + lane + 64 * r] = (bcpi >> r) & 1u ? c : 0.0;
       }
     }
     LDS_FENCE();
@@ -1238,16 +1271,24 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       fwd_ready = true;
     }
 #endif
-    // x, z, y updates (auxil.c update_x / update_z / update_y)
+    // x, z, y updates (auxil.c update_x / update_z / update_y).  The solution reads are issued
+    // together before any use (otherwise the compiler reuses one register pair for all of them
+    // and waits for each read in turn)
+    double wx[RN], wz[RM];
+#pragma unroll
+    for (int r = 0; r < RN; ++r) wx[r] = v[wsx[r]];  // the junk slot reads back 0
+#pragma unroll
+    for (int r = 0; r < RM; ++r) wz[r] = v[wsz[r]];
+    __builtin_amdgcn_sched_group_barrier(0x100, RN + RM, 0);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
-      const double xt = v[wsx[r]];  // the junk slot reads back 0
+      const double xt = wx[r];
       S.x[r] = alpha * xt + alpha_c * xp[r];
       dx[r] = S.x[r] - xp[r];
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
-      const double nu = v[wsz[r]];
+      const double nu = wz[r];
       const double ri = rinv_of(S, r);
       const double zt = bz[r] + ri * nu;
       const double zr = alpha * zt + alpha_c * zp[r];
@@ -1588,7 +1629,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
            o_eTk = push_blob(blob, pl.ellAt.pk), o_ePk = push_blob(blob, pl.ellP.pk),
            o_eAq = push_blob(blob, pl.ellA.sk), o_eTq = push_blob(blob, pl.ellAt.sk),
            o_ePq = push_blob(blob, pl.ellP.sk), o_sra = push_blob(blob, pl.sra),
-           o_sca = push_blob(blob, pl.sca), o_wc = push_blob(blob, pl.wcopy);
+           o_sca = push_blob(blob, pl.sca), o_wc = push_blob(blob, pl.wcopy),
+           o_bc = push_blob(blob, pl.bcopy);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
@@ -1603,6 +1645,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
     dp.wsx = (const uint16_t*)(b + o_wx), dp.wsz = (const uint16_t*)(b + o_wz);
     dp.wcopy = (const uint32_t*)(b + o_wc);
+    dp.bcopy = (const uint32_t*)(b + o_bc);
     dp.Ap = (const uint16_t*)(b + o_Ap), dp.Ai = (const uint16_t*)(b + o_Ai);
     dp.Acol = (const uint16_t*)(b + o_Ac), dp.Arp = (const uint16_t*)(b + o_Arp);
     dp.Ark = (const uint16_t*)(b + o_Ark), dp.Arj = (const uint16_t*)(b + o_Arj);

@@ -151,6 +151,11 @@ struct Plan {
   // the first block with an empty reach, whose forward-solve output is its right-hand side
   // (W_r = C_r): the right-hand side pass stores it into W directly and no solve task computes it
   std::vector<uint32_t> wcopy;
+  // the same for the backward solve, per lane, bit r: W slot lane + 64 r (physical slot order of the
+  // diagonal pass) holds a backward copy row, whose W starts at (1/D) W instead of 0; bcopy_row marks
+  // them by permuted row (construction order; finish_copy_masks maps them to physical slots)
+  std::vector<uint32_t> bcopy;
+  std::vector<uint8_t> bcopy_row;
   bool paired = true;  // solve-step kind (build_plan)
   // schedules (STEP_WORDS words per step): factorization of U = L D and D by levels, then
   // (after the flat pass L = U * (1/D)_col) the block-inverse tail; forward and backward solves
@@ -169,8 +174,13 @@ struct Plan {
   // ellP's: the per-instance scaled values live only in the ELL copies
   std::vector<uint16_t> posA, posP;
   int levels_fwd = 0, levels_bwd = 0;
+  std::vector<int> fwd_level_steps, bwd_level_steps;  // solve steps of each level (diagnostics)
   std::string error;
 };
+
+// Physical-slot masks of the diagonal pass (Plan::bcopy) from Plan::bcopy_row and the final slot
+// maps wsx / wsz: call after the layout is final (build_plan_tuned does).
+void finish_copy_masks(Plan& plan);
 
 // Builds the plan; returns false (with plan.error set) if the structure is unsupported.
 // capM / capW: per block, max entries of the block inverse and max solve terms of its w-tasks.

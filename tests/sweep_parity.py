@@ -88,7 +88,14 @@ def compare(a, b):
     ia, ib = a[:, IDX["i_term"]], b[:, IDX["i_term"]]
     fa, fb = a[:, IDX["final_err"]], b[:, IDX["final_err"]]
     same_run = (sa == sb) & (ia == ib) & (np.abs(fa - fb) <= 1e-6 * (1 + np.abs(fb)))
-    return dict(scenarios=int(a.shape[0]),
+    # sampling noise of the differences of the reported statistics: paired bootstrap over the
+    # scenarios (the same resampled chasers on both sides), standard error of the difference
+    rng = np.random.default_rng(12345)
+    idx = rng.integers(0, a.shape[0], size=(1000, a.shape[0]))
+    se = dict(final_err_median=float(np.std(np.median(fa[idx], 1) - np.median(fb[idx], 1))),
+              i_term_mean=float(np.std(ia[idx].mean(1) - ib[idx].mean(1))),
+              success_rate=float(np.std(sa[idx].mean(1) - sb[idx].mean(1))))
+    return dict(scenarios=int(a.shape[0]), se=se,
                 success_rate=(float(sa.mean()), float(sb.mean())),
                 success_agree=float(np.mean(sa == sb)),
                 i_term_agree=float(np.mean(ia == ib)),

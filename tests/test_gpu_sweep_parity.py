@@ -36,8 +36,9 @@ def test_full_length_sweep_matches_oracle_driven_runs(scenario, nx, noise, rejec
     assert ev["same_run"] >= fl["same_run"] - 12 / G, (ev, fl)
     assert ev["i_term_agree"] >= fl["i_term_agree"] - 12 / G, (ev, fl)
     assert ev["success_agree"] >= fl["success_agree"] - 3 / G, (ev, fl)
-    # the statistics a sweep reports
-    assert abs(ev["success_rate"][0] - ev["success_rate"][1]) <= 4 / G, ev
-    assert abs(ev["i_term_mean"][0] - ev["i_term_mean"][1]) <= 0.06 * ev["i_term_mean"][1], ev
-    assert abs(ev["final_err_median"][0] - ev["final_err_median"][1]) <= \
-        0.1 * ev["final_err_median"][1], ev
+    # the statistics a sweep reports differ by no more than their own sampling noise: three
+    # standard errors of the paired difference (bootstrap over the scenarios, sweep_parity.compare)
+    # -- the oracle against itself moved the median final error by 6.8 % on the radial case
+    for key in ("success_rate", "i_term_mean", "final_err_median"):
+        d = abs(ev[key][0] - ev[key][1])
+        assert d <= 3 * ev["se"][key] + 1e-12, (key, d, ev["se"][key], ev)

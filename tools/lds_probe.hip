@@ -18,6 +18,17 @@ __global__ void __launch_bounds__(64) probe(double* out, int iters) {
   __syncthreads();
   const uint32_t base = (uint32_t)(uintptr_t)lds + lane * 8;
   double acc = 0.0;
+  // opaque per-slot addresses (as the engine's records): stops the compiler from merging two
+  // reads into one ds_read2st64_b64
+  uint32_t ad[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    ad[k] = base + 512u * k;
+    asm volatile("" : "+v"(ad[k]));
+  }
+  double mat[8], mat2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) mat[k] = lds[lane + 64 * k], mat2[k] = 0.0;
 #pragma unroll 1
   for (int i = 0; i < iters; ++i) {
     if constexpr (MODE == 0) {  // 16 independent reads
@@ -35,31 +46,32 @@ __global__ void __launch_bounds__(64) probe(double* out, int iters) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) *(lds_double*)(size_t)(base + 512u * k) = acc + k;
       acc += 1.0;
-    } else if constexpr (MODE >= 4) {  // solve-step variants (see names[])
+    } else if constexpr (MODE >= 4 && MODE <= 9) {  // solve-step variants (see names[])
       // 4: 16 reads + 3 writes; 5: 16 reads + 2 atomics; 6: 4 b128 + 8 b64 reads + 3 atomics;
-      // 7: 16 reads + 4 atomics; 8: 16 reads + 1 atomic; 9: 8 reads + 3 atomics
+      // 7: 16 reads + 4 atomics; 8: 16 reads + 1 atomic; 9: 8 reads + 3 atomics, the other 8
+      // operands (matrix values) from registers
       double x[16];
       if constexpr (MODE == 6) {
         typedef double d2 __attribute__((ext_vector_type(2)));
         typedef __attribute__((address_space(3))) d2 lds_d2;
-        const uint32_t b2 = (uint32_t)(uintptr_t)lds + lane * 16;
+        const uint32_t b2 = (uint32_t)(uintptr_t)lds + lane * 16;  // b128 pairs: conflict-free
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const d2 v = *(lds_d2*)(size_t)(b2 + 1024u * k);
           x[2 * k] = v.x, x[2 * k + 1] = v.y;
         }
 #pragma unroll
-        for (int k = 8; k < 16; ++k) x[k] = *(lds_double*)(size_t)(base + 512u * k);
+        for (int k = 8; k < 16; ++k) x[k] = *(lds_double*)(size_t)ad[k];
         __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
       } else if constexpr (MODE == 9) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = *(lds_double*)(size_t)(base + 512u * k);
+        for (int k = 8; k < 16; ++k) x[k] = *(lds_double*)(size_t)ad[k];
 #pragma unroll
-        for (int k = 8; k < 16; ++k) x[k] = x[k - 8] * 0.5;
+        for (int k = 0; k < 8; ++k) x[k] = mat[k];  // matrix operands held in registers
         __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
       } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = *(lds_double*)(size_t)(base + 512u * k);
+        for (int k = 0; k < 16; ++k) x[k] = *(lds_double*)(size_t)ad[k];
         __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
@@ -68,13 +80,13 @@ __global__ void __launch_bounds__(64) probe(double* out, int iters) {
       const double n2 = fma(-x[5], x[13], -(x[4] * x[12]));
       const double n3 = fma(-x[7], x[15], -(x[6] * x[14]));
       auto add = [&](int slot, double v) {
-        __hip_atomic_fetch_add((lds_double*)(size_t)(base + 512u * slot), v, __ATOMIC_RELAXED,
+        __hip_atomic_fetch_add((lds_double*)(size_t)ad[slot], v, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
       };
       if constexpr (MODE == 4) {
-        *(lds_double*)(size_t)(base + 512u * 16) = n0 + n1;
-        *(lds_double*)(size_t)(base + 512u * 17) = n2;
-        *(lds_double*)(size_t)(base + 512u * 18) = n3;
+        *(lds_double*)(size_t)ad[16] = n0 + n1;
+        *(lds_double*)(size_t)ad[17] = n2;
+        *(lds_double*)(size_t)ad[18] = n3;
       } else if constexpr (MODE == 5) {
         add(16, n0 + n1), add(17, n2 + n3);
       } else if constexpr (MODE == 7) {
@@ -85,25 +97,53 @@ __global__ void __launch_bounds__(64) probe(double* out, int iters) {
         add(16, n0 + n1), add(17, n2), add(18, n3);
       }
       asm volatile("" ::: "memory");
+    } else if constexpr (MODE == 10) {
+      // split step: the 8 operands the previous step's atomics cannot have written (the matrix
+      // values) are read one step ahead, issued between this step's 8 dependent reads and its
+      // products; the dependent reads follow the previous step's atomics.  Two steps per trip
+      // (register sets mat / mat2 alternate), so no moves.
+      auto step = [&](const double(&cur)[8], double(&nxt)[8]) {
+        double y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y[k] = *(lds_double*)(size_t)ad[8 + k];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nxt[k] = *(lds_double*)(size_t)ad[k];
+        __builtin_amdgcn_sched_barrier(0);
+        const double n0 = fma(-cur[1], y[1], -(cur[0] * y[0])) + fma(-cur[3], y[3], -(cur[2] * y[2]));
+        const double n2 = fma(-cur[5], y[5], -(cur[4] * y[4]));
+        const double n3 = fma(-cur[7], y[7], -(cur[6] * y[6]));
+        __hip_atomic_fetch_add((lds_double*)(size_t)ad[16], n0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add((lds_double*)(size_t)ad[17], n2, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add((lds_double*)(size_t)ad[18], n3, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      step(mat, mat2);
+      step(mat2, mat);
+      ++i;
     } else {  // one solve step: 16 reads, 8 products, 3 atomics; the next step reads behind them
       double x[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) x[k] = *(lds_double*)(size_t)(base + 512u * k);
+      for (int k = 0; k < 16; ++k) x[k] = *(lds_double*)(size_t)ad[k];
       __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
       const double n0 = fma(-x[1], x[9], -(x[0] * x[8])) + fma(-x[3], x[11], -(x[2] * x[10]));
       const double n2 = fma(-x[5], x[13], -(x[4] * x[12]));
       const double n3 = fma(-x[7], x[15], -(x[6] * x[14]));
-      __hip_atomic_fetch_add((lds_double*)(size_t)(base + 512u * 16), n0, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add((lds_double*)(size_t)ad[16], n0, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add((lds_double*)(size_t)(base + 512u * 17), n2, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add((lds_double*)(size_t)ad[17], n2, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add((lds_double*)(size_t)(base + 512u * 18), n3, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add((lds_double*)(size_t)ad[18], n3, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
       asm volatile("" ::: "memory");
     }
   }
-  out[blockIdx.x * 64 + lane] = acc + lds[lane];
+  out[blockIdx.x * 64 + lane] = acc + lds[lane] + mat[lane & 7] + mat2[lane & 7];
 }
 
 int main() {
@@ -113,13 +153,13 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int iters = 4000;
-  const char* names[10] = {"ds_read_b64 x16", "ds_add_f64 x16", "ds_write_b64 x16", "solve step",
+  const char* names[11] = {"ds_read_b64 x16", "ds_add_f64 x16", "ds_write_b64 x16", "solve step",
                            "step 16r+3w", "step 16r+2a", "step 4q+8r+3a", "step 16r+4a",
-                           "step 16r+1a", "step 8r+3a"};
+                           "step 16r+1a", "step 8r+8reg+3a", "step split 8+8r+3a"};
   typedef void (*kfn)(double*, int);
-  const kfn ks[10] = {probe<0>, probe<1>, probe<2>, probe<3>, probe<4>,
-                      probe<5>, probe<6>, probe<7>, probe<8>, probe<9>};
-  for (int mode = 0; mode < 10; ++mode) {
+  const kfn ks[11] = {probe<0>, probe<1>, probe<2>, probe<3>, probe<4>, probe<5>,
+                      probe<6>, probe<7>, probe<8>, probe<9>, probe<10>};
+  for (int mode = 0; mode < 11; ++mode) {
     for (int wpc : {1, 2, 4, 8}) {
       const int lds = (160 * 1024) / wpc / 16 * 16;
       const int blocks = 256 * wpc;
