@@ -166,7 +166,8 @@ def load_profile(name, B, nx, split):
     return None
 
 
-def closed_loop_run(prob, X0, B, K, W, S, eps, rank, device, dist=None, track=None):
+def closed_loop_run(prob, X0, B, K, W, S, eps, rank, device, dist=None, track=None,
+                    longest_first=False):
     """The timed closed loop: S shards of the B chasers on concurrent HIP streams, one cold solve
     (step 0, timed on its own), W - 1 more untimed warm steps, K timed warm steps bracketed by
     barrier + synchronize.  Per step and chaser it keeps the iterations, status and whether the
@@ -180,7 +181,8 @@ def closed_loop_run(prob, X0, B, K, W, S, eps, rank, device, dist=None, track=No
     for j in range(S):
         st_j = torch.cuda.Stream(device=device) if S > 1 else None
         cls.append(BatchClosedLoop(prob, X0[cut[j]:cut[j + 1]], device=device, eps_abs=eps,
-                                   eps_rel=eps, stream=st_j, id_offset=rank * B + cut[j]))
+                                   eps_rel=eps, stream=st_j, id_offset=rank * B + cut[j],
+                                   longest_first=longest_first))
         if track:
             cls[-1].enable_tracking(*track)
     torch.cuda.synchronize()
@@ -314,6 +316,7 @@ def bench_discrete(args, rank, world, device, dist):
     B, K, S = args.batch, args.steps, max(1, min(args.split, args.batch))
     X0 = initial_states(world * B, rank, B, args.seed)
     run = closed_loop_run(prob, X0, B, K, args.warmup, S, args.eps, rank, device, dist,
+                          longest_first=args.order == "iters",
                           track=(int(sim.T_final / sim.time_stp), *sim.suc_cond))
     cls = run["cls"]
     elapsed = run["elapsed"]
@@ -414,7 +417,8 @@ def bench_config3(args, rank, device):
     prob = qp_model.build_problem(sim, mpc, fail, deb)
     B, K, W, S = args.batch, args.config3_steps, 3, max(1, min(args.split, args.batch))
     X0 = initial_states(B, 0, B, args.seed)
-    run = closed_loop_run(prob, X0, B, K, W, S, args.eps, rank, device, None, track=None)
+    run = closed_loop_run(prob, X0, B, K, W, S, args.eps, rank, device, None, track=None,
+                          longest_first=args.order == "iters")
     it, act = run["it"], run["act"]
     roof = roofline(run, S, K, run["elapsed"])
     attach_profiles(roof, B, 40, S, K, run["elapsed"])
@@ -458,7 +462,7 @@ def bench_continuous(args, rank, world, device, dist):
     X0 = initial_states(world * B, rank, B, args.seed)
     cl = BatchClosedLoopC(prob, X0, T_cont=0.001, T_final=300, mean_motion=sim.mean_mtn,
                           isDeltaV=args.dv, device=device, noise=noise, id_offset=rank * B,
-                          eps_abs=args.eps, eps_rel=args.eps)
+                          eps_abs=args.eps, eps_rel=args.eps, longest_first=args.order == "iters")
     for _ in range(W):
         cl.period()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
@@ -539,6 +543,9 @@ def main(argv=None):
     ap.add_argument("--config3-steps", type=int, default=10)
     ap.add_argument("--continuous", action="store_true",
                     help="BASELINE config 4: the continuous-time nonlinear loop (default N=40)")
+    ap.add_argument("--order", choices=("iters", "none"), default="none",
+                    help="solve order of each launch: longest-first by the chaser's last ADMM "
+                         "iterations (mpcqp_set_order) or instance order")
     ap.add_argument("--split", type=int, default=2,
                     help="chaser shards per GPU on concurrent HIP streams (fills one shard's solve "
                          "tail with the other shard's work; 2 measured best, 4 no better than 1)")

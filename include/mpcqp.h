@@ -137,6 +137,13 @@ int mpcqp_copy_data(mpcqp_handle *h, double *Ax, double *l, double *u);
  * closed loops passes its `done` flags, so chasers whose run has terminated cost nothing (the
  * reference stops calling solve() at termination, src/trajectorySimulate.py:288-296). */
 int mpcqp_set_skip(mpcqp_handle *h, const int32_t *skip);
+/* Solve order (device pointer, kept by the handle; NULL = instance order): a permutation of the B
+ * instance ids, handed to the persistent waves in this order by the work counter.  Results are
+ * unchanged (instances are independent); only the packing of the launch changes.  A closed loop
+ * passes its chasers longest-first by the last solve's ADMM iterations, so the instances that run
+ * to max_iter start first and the launch ends on short ones (no reference counterpart: OSQP solves
+ * one problem at a time). */
+int mpcqp_set_order(mpcqp_handle *h, const int32_t *order);
 
 /* Copy the warm-start state the handle carries between solves (what OSQP keeps inside its
  * workspace) into caller device buffers (any may be NULL): the SCALED iterates xs [B*n], zs, ys

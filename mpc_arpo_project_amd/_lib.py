@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("MPCQP_LIBRARY") or os.path.join(_HERE, "libmpcqp.so")
 EXPORTED = (
     "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",
     "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
-    "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_get_state", "mpcqp_set_state", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
+    "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_set_order", "mpcqp_get_state", "mpcqp_set_state", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
     "mpcqp_schedule_check",
     "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind", "mpcqp_schedule_kind",
     "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
@@ -120,6 +120,7 @@ def lib():
     L.mpcqp_get_state.argtypes = [vp, dp, dp, dp, dp, dp]
     L.mpcqp_set_state.argtypes = [vp, dp, dp, dp, dp, dp]
     L.mpcqp_set_skip.argtypes = [vp, dp]
+    L.mpcqp_set_order.argtypes = [vp, dp]
     L.mpcqp_data_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
     L.mpcqp_schedule_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
     L.mpcqp_export_symbolic.argtypes = [vp, i32p, i32p, i32p]

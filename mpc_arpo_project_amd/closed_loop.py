@@ -90,7 +90,7 @@ class BatchClosedLoop:
     """
 
     def __init__(self, prob: MPCProblem, x0, device="cuda", noise=None, noise_seed=123,
-                 id_offset=0, noise_source=None, **settings):
+                 id_offset=0, noise_source=None, longest_first=False, **settings):
         x0 = np.asarray(x0, dtype=float)
         if x0.ndim != 2 or x0.shape[1] != 4:
             raise ValueError("x0 must have shape (B, 4)")
@@ -126,6 +126,16 @@ class BatchClosedLoop:
         self._bufs = data_buffers(self.qp)
         # terminated chasers are not solved again (the reference leaves its loop at termination)
         self.qp.set_skip(self.done)
+        # solve order (longest_first=True): every step after the first hands the chasers to the
+        # persistent launch longest-first by their last solve's ADMM iterations (a warm closed
+        # loop's best predictor of the next), so the max_iter runs start first and the launch ends
+        # on short solves (results unchanged, mpcqp_set_order).  Off by default: on the bench it
+        # measured 896k vs 895k solves/s with two shards and 798k vs 807k with one
+        # (profiles/r03/ab_order.txt) -- the launch's tail is not where the time goes
+        self._order = None
+        if longest_first:
+            self._order = torch.arange(self.B, dtype=torch.int32, device=self.device)
+            self.qp.set_order(self._order)
         self.u0 = prob.u0_slice.start
         self.steps = 0
         check(_lib.lib().mpcqp_cl_set_ids(self._cl, int(id_offset)), "mpcqp_cl_set_ids")
@@ -225,11 +235,18 @@ class BatchClosedLoop:
                 u = r.x[:, self.u0:self.u0 + 2]
                 self.u0_first.copy_(torch.where(active[:, None], u, self.u0_first))
 
+    def _reorder(self, r):
+        """next solve's order: longest-first by this solve's ADMM iterations (engine stream)"""
+        if self._order is not None:
+            with torch.cuda.stream(self.qp.stream):
+                self._order.copy_(torch.argsort(r.iter, descending=True))
+
     def step_after_solve(self, r):
         """Controller select + plant + QP-data rebuild for a solve already enqueued (async)."""
         L = _lib.lib()
         if getattr(self, "_tracking", False):
             self._track_solve(r)
+        self._reorder(r)
         opt = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         rc = L.mpcqp_cl_step(self._cl, r.status.data_ptr(), r.x.data_ptr(), self.qp.n, self.u0,
                              self.x_true.data_ptr(), self.ctrl_prev.data_ptr(),
@@ -424,6 +441,7 @@ class BatchClosedLoopC(BatchClosedLoop):
         r = self.qp.solve_async()
         if on_solved is not None:
             on_solved(self.qp.stream)
+        self._reorder(r)
         L = _lib.lib()
         opt = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         if traj is not None and (tuple(traj.shape) != (self.B, nsub, 4) or

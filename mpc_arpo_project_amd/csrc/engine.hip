@@ -86,6 +86,7 @@ struct KParams {
   // backend of ROCm 7.2 was seen to spill such a hoisted double and reload only its low half)
   double rho0;
   const int32_t* skip;  // [B] or null: instances with skip[i] != 0 are not solved (outputs kept)
+  const int32_t* order;  // [B] or null: the k-th instance handed out is order[k] (mpcqp_set_order)
 };
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
@@ -208,21 +209,6 @@ __device__ __forceinline__ void load_solve(Rsrc rs, int soff, uint32_t lane, Sol
       __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + 4 * SOLVE_TERM_WORDS, soff, 0);
   r.t0 = tg[0], r.t1 = tg[1], r.t2 = tg[2], r.t3 = tg[3];
 }
-#ifdef EXP_AGPR
-__device__ __forceinline__ uint32_t agpr_rt(uint32_t x) {
-  uint32_t a, v;
-  asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(a) : "v"(x));
-  asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(a));
-  return v;
-}
-__device__ __forceinline__ void agpr_reload(SolveRec& r) {
-#pragma unroll
-  for (int c = 0; c < SOLVE_MAXC; ++c) r.a[c] = agpr_rt(r.a[c]), r.b[c] = agpr_rt(r.b[c]);
-  r.t0 = agpr_rt(r.t0), r.t2 = agpr_rt(r.t2), r.t3 = agpr_rt(r.t3);
-}
-template <typename R>
-__device__ __forceinline__ void agpr_reload(R&) {}
-#endif
 // one lane's records of a factorization step: meta word + FAC_MAXC (a, b, c, -) address quads
 struct FacRec {
   uint32_t mt;
@@ -340,24 +326,12 @@ __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops
 // The rotation is unrolled 12 steps deep: LLVM's waitcnt insertion merges states pessimistically
 // at a loop header (the first step after it would wait for all three sets), so the header is
 // reached at most once per ~12 steps.
-#if defined(EXP_NOREC)
-#define MPCQP_STEP(X)                                       \
-  ops.step(p.X, s);                                         \
-  if (++s >= n) break;
-#elif defined(EXP_AGPR)
-// ablation: the records of step s + 2 re-read from AGPR copies (19 v_accvgpr_read), no VMEM
-#define MPCQP_STEP(X)                                       \
-  ops.step(p.X, s);                                         \
-  if (++s >= n) break;                                      \
-  agpr_reload(p.X);
-#else
 #define MPCQP_STEP(X)                                       \
   ops.step(p.X, s);                                         \
   if (++s >= n) break;                                      \
   __builtin_amdgcn_sched_barrier(0);                        \
   Ops::load(rs, step_off<Ops>(n, s + 2), lane, p.X);        \
   __builtin_amdgcn_sched_barrier(0);
-#endif
 template <typename Ops>
 __device__ __forceinline__ void run_body(Rsrc rs, int n, uint32_t lane, const Ops& ops,
                                          Pipe<Ops>& p) {
@@ -1252,9 +1226,9 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         dv[r] = v[P.DINV + lane + 64 * r];
       }
 #pragma unroll
-      for (int r = 0; r < RN + RM; ++r) {
+      for (int r = 0; r < RN + RM; ++r) {  // C at the immediate distance coff: one ds_write2st64
         const double c = wv[r] * dv[r];
-        v[P.CACC + lane + 64 * r] = c;
+        v[P.W + lane + 64 * r + coff] = c;
         v[P.W + lane + 64 * r] = (bcpi >> r) & 1u ? c : 0.0;
       }
     }
@@ -1446,6 +1420,10 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
     inst = (unsigned int)__shfl((int)inst, 0);
     inst = __builtin_amdgcn_readfirstlane(inst);
     if (inst >= (unsigned int)p.B) break;
+    if (p.order) {
+      inst = __builtin_amdgcn_readfirstlane((unsigned int)p.order[inst]);
+      if (inst >= (unsigned int)p.B) continue;  // not a permutation entry: nothing to solve
+    }
     if (p.skip && p.skip[inst]) continue;  // wave-uniform
     // larger buckets: an opaque copy of the lane id per instance, so per-lane address arithmetic
     // is not hoisted out of the instance loop (held in registers for the whole kernel it spills)
@@ -1519,7 +1497,8 @@ struct mpcqp_handle {
   unsigned int* counter = nullptr;
   unsigned long long* timing = nullptr;  // MPCQP_TIMING builds
   bool has_data = false;
-  const int32_t* skip = nullptr;  // mpcqp_set_skip
+  const int32_t* skip = nullptr;   // mpcqp_set_skip
+  const int32_t* order = nullptr;  // mpcqp_set_order
   int grid = 0, lds_bytes = 0, waves_per_cu = 0;
   kernel_fn kern = nullptr;
 };
@@ -1674,6 +1653,9 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.S_ZERO = pl.S_ZERO;
     dp.MV = pl.MV, dp.MVZ = pl.MVZ;
     dp.sra = (const uint16_t*)(b + o_sra), dp.sca = (const uint16_t*)(b + o_sca), dp.SJ = pl.SJ;
+    // the vector passes address C through W's slot plus the compile-time distance 64 (RN + RM)
+    if (pl.CACC - pl.W != pl.NKP || pl.NKP != 64 * (pl.RN + pl.RM))
+      return cleanup_fail(MPCQP_E_INVALID, "internal: C region not at the kernel's distance from W");
     if (pl.SJ > 8 * pl.RN)  // the kernel holds 8 RN row / column slots per lane (scale_problem)
       return cleanup_fail(MPCQP_E_UNSUPPORTED, "too many matrix values for the scaling registers");
 
@@ -1802,6 +1784,7 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   p.timing = h->timing;
   p.rho0 = std::min(std::max(h->set.rho, RHO_MIN), RHO_MAX);
   p.skip = h->skip;
+  p.order = h->order;
   HIPCHK(hipMemsetAsync(h->counter, 0, 64, h->stream));
   hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(64), h->lds_bytes, h->stream, p);
   HIPCHK(hipGetLastError());
@@ -1843,6 +1826,12 @@ int mpcqp_copy_data(mpcqp_handle* h, double* Ax, double* l, double* u) {
 int mpcqp_set_skip(mpcqp_handle* h, const int32_t* skip) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");
   h->skip = skip;
+  return 0;
+}
+
+int mpcqp_set_order(mpcqp_handle* h, const int32_t* order) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  h->order = order;
   return 0;
 }
 

@@ -184,6 +184,18 @@ class BatchQP:
               "mpcqp_set_skip")
         self._skip = mask
 
+    def set_order(self, order):
+        """int32 device tensor [B] (kept alive by the handle) or None: a permutation of the
+        instance ids, the order in which the persistent launch takes instances (results unchanged;
+        mpcqp_set_order).  The tensor is read at every solve, so it may be rewritten in place."""
+        if order is not None:
+            if order.dtype != torch.int32 or tuple(order.shape) != (self.B,) or \
+                    not order.is_cuda or not order.is_contiguous():
+                raise ValueError(f"order must be a contiguous int32 tensor of shape ({self.B},)")
+        check(_lib.lib().mpcqp_set_order(self._h, None if order is None else order.data_ptr()),
+              "mpcqp_set_order")
+        self._order = order
+
     def get_state(self):
         """Warm-start state carried to the next solve (scaled xs, zs, ys; rho; has_state), as new
         device tensors -- the white-box hook the oracle's `state()` mirrors."""

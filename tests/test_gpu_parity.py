@@ -154,3 +154,36 @@ def test_repeated_solves_are_bit_identical(golden):
             assert np.array_equal(r.x.cpu().numpy()[0], runs[0][2][b], equal_nan=True)
         for k in range(3):
             assert np.array_equal(runs[0][k], runs[1][k], equal_nan=True)
+
+
+def test_solve_order_does_not_change_results(golden):
+    """mpcqp_set_order only changes which wave takes which instance: a random permutation gives
+    bit-identical statuses, iterations and solutions, with and without a skip mask"""
+    from conftest import problem
+
+    prob = problem(20, False)
+    d = golden("batch_n20")
+    B = 64
+    st = dict(eps_abs=1e-4, eps_rel=1e-4)
+    outs = []
+    for mode in ("none", "perm", "perm+skip"):
+        qp = BatchQP(prob.P, prob.A, batch=B, **st)
+        qp.set_data(q=prob.q, Ax=d["Ax"][:B], l=d["l"][:B], u=d["u"][:B])
+        if mode != "none":
+            g = torch.Generator().manual_seed(5)
+            qp.set_order(torch.randperm(B, generator=g).to(torch.int32).to(qp.device))
+        if mode == "perm+skip":
+            skip = torch.zeros(B, dtype=torch.int32, device=qp.device)
+            skip[::7] = 1
+            qp.set_skip(skip)
+        r = qp.solve()
+        outs.append((r.status.cpu().numpy(), r.iter.cpu().numpy(), r.x.cpu().numpy()))
+        qp.close()
+    for k in range(3):
+        assert np.array_equal(outs[0][k], outs[1][k], equal_nan=True)
+    solved = np.ones(B, dtype=bool)
+    solved[::7] = False
+    for k in range(3):
+        assert np.array_equal(outs[0][k][solved], outs[2][k][solved], equal_nan=True)
+    with pytest.raises(ValueError):
+        BatchQP(prob.P, prob.A, batch=4, **st).set_order(torch.zeros(3, dtype=torch.int32))
