@@ -303,12 +303,7 @@ struct Pipe {
 };
 template <typename Ops>
 __device__ __forceinline__ int step_off(int n, int s) {
-#ifdef MPCQP_OOR_TAIL
-  (void)n;
-  return s * (Ops::STRIDE * 4);  // past the table: the buffer's range check returns zeros
-#else
   return (s < n ? s : n - 1) * (Ops::STRIDE * 4);
-#endif
 }
 template <typename Ops>
 __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops>& p) {
@@ -1173,18 +1168,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   const SolveOps<PAIRED> sops{v};
   const Rsrc rs_fwd = table_rsrc(P.fwd, P.nfwd, SOLVE_STEP_WORDS);
   const Rsrc rs_bwd = table_rsrc(P.bwd, P.nbwd, SOLVE_STEP_WORDS);
-#ifdef MPCQP_EARLY_FWD
-  bool fwd_ready = false;
-#endif
   for (iter = 1; iter <= p.s.max_iter; ++iter) {
     T_COUNT(T_ITERS);
     T_BEGIN(t_v0);
-#ifdef MPCQP_EARLY_FWD
-    if (!fwd_ready) prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);
-    fwd_ready = false;
-#else
     prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);  // lands while the right-hand side is formed
-#endif
     double xp[RN], zp[RM], bz[RM];
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
     // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
@@ -1239,12 +1226,6 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
     T_END(T_BWD, t_bw);
     T_BEGIN(t_v2);
-#ifdef MPCQP_EARLY_FWD
-    if (chk_left != 1 && ar_left != 1) {  // no check / rho adaptation after this iteration
-      prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);
-      fwd_ready = true;
-    }
-#endif
     // x, z, y updates (auxil.c update_x / update_z / update_y).  The solution reads are issued
     // together before any use (otherwise the compiler reuses one register pair for all of them
     // and waits for each read in turn)

@@ -3,7 +3,10 @@ the derived LDS utilisation (MI355X_MICROARCH.md: SQ_LDS_IDX_ACTIVE = LDS-array 
 SQ_LDS_BANK_CONFLICT = their conflict part; SQ_* wave counters in quad-cycles; GRBM_GUI_ACTIVE
 summed over the 8 XCDs).
 
-    python tools/sq_summary.py DIR [DIR ...] > summary.json
+    python tools/sq_summary.py [--kernel NAME] DIR [DIR ...] > summary.json
+
+--kernel: substring of the kernel name (default qp_batch_kernel; "qp_batch_kernel<2, 4" keeps the
+N = 20 launches when a run also holds the config-3 leg's N = 40 ones)
 """
 import csv
 import glob
@@ -14,11 +17,15 @@ import sys
 
 def main():
     vals = {}
-    for d in sys.argv[1:]:
+    args = sys.argv[1:]
+    kernel = "qp_batch_kernel"
+    if args and args[0] == "--kernel":
+        kernel, args = args[1], args[2:]
+    for d in args:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             per = {}
             for r in csv.DictReader(open(f)):
-                if "qp_batch_kernel" not in r["Kernel_Name"]:
+                if kernel not in r["Kernel_Name"]:
                     continue
                 key = (r["Counter_Name"], int(r["Dispatch_Id"]))
                 per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
