@@ -118,8 +118,11 @@ int pack_fac_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<u
       const size_t base = tbl.size();
       tbl.resize(base + FAC_STEP_WORDS, zb);
       uint32_t* st = tbl.data() + base;
+      bool anyD = false;
+      for (auto& pr : in) anyD = anyD || pr.second->t->isD;
       for (int l = 0; l < 64; ++l)
-        st[l] = ((uint32_t)C << META_C_SHIFT) | ((uint32_t)glog << META_SGLOG_SHIFT);
+        st[l] = ((uint32_t)C << META_C_SHIFT) | ((uint32_t)glog << META_SGLOG_SHIFT) |
+                (anyD ? META_SISD : 0u);
       for (auto& pr : in) {
         const int off = pr.first;
         const Placed* p = pr.second;

@@ -53,6 +53,7 @@ constexpr uint32_t META_HEAD = 1u << 20;
 constexpr uint32_t META_ISD = 1u << 21;       // factorization: target is D_j -> also write 1/D_j
 constexpr int META_C_SHIFT = 22;              // 4 bits: terms per lane in this step
 constexpr int META_SGLOG_SHIFT = 26;          // 3 bits: widest group log2 in this step
+constexpr uint32_t META_SISD = 1u << 29;      // step-wide: some lane of this step stores a 1/D_j
 
 // Sparse mat-vec in padded per-slot ELL form for the residual checks: output element e sits on
 // lane e % 64, register slot r = e / 64; every used slot has exactly KMAX terms per lane (compile-
