@@ -1353,6 +1353,8 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
   key.push_back(n), key.push_back(m), key.push_back(lds_per_cu), key.push_back(max_per_cu);
   key.push_back(anneal);
   key.push_back(fp ? atoi(fp) : -1);
+  const char* cm = getenv("MPCQP_COPY_ROWS");  // diagnostics: the copy-row mode (build_plan)
+  key.push_back(cm ? atoi(cm) : -1);
   key.insert(key.end(), Pp, Pp + n + 1);
   key.insert(key.end(), Pi, Pi + Pp[n]);
   key.insert(key.end(), Ap, Ap + n + 1);

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Profile evidence at HEAD (GPU box): default bench with the CPU baseline; rocprofv3 kernel trace of
 # the default workload; PMC passes (FETCH_SIZE / WRITE_SIZE with calibration, SQ LDS counters); the
-# N=40 impulsive delta-v bench (BASELINE config 3) with its kernel trace.   usage: tools/profile.sh <tag>
+# N=40 impulsive delta-v bench (BASELINE config 3) with its kernel trace; the continuous-time loop
+# (config 4) with its kernel trace.   usage: tools/profile.sh <tag>
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-prof}"; mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
@@ -20,3 +21,5 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU
 echo sq ok
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace40" -o run -- $B --nx 40 --dv > "$O/bench40.json" 2> "$O/bench40.err" || { echo n40 failed; tail -5 "$O/bench40.err"; exit 1; }
 echo "n40: $(head -c 300 $O/bench40.json)"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_cont" -o run -- python3 $R/bench.py --continuous --steps 5 --warmup 1 > "$O/bench_cont.json" 2> "$O/bench_cont.err" || { echo continuous trace failed; tail -5 "$O/bench_cont.err"; exit 1; }
+echo "continuous: $(head -c 300 $O/bench_cont.json)"
