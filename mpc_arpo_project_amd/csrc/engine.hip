@@ -4,11 +4,13 @@
 //   * one QP instance per wavefront (64 lanes, one wave per workgroup), persistent grid sized to
 //     the resident-wave capacity; waves pull instance ids from an atomic work counter, so the
 //     heavy-tailed ADMM iteration counts balance themselves;
-//   * the instance's KKT factor L, 1/D and the solve vector live in LDS (16 KB at N = 20), the
-//     primal/dual iterates, bounds and scalings live in VGPRs (element i on lane i % 64, slot
-//     i / 64); scaled P/A values are parked in a per-wave scratch slab that stays L2-resident;
-//   * numeric factorization and both triangular solves are driven by host-compiled level
-//     schedules (symbolic.hpp): each step is a 64-lane dot-product/butterfly pass over LDS;
+//   * the instance's image lives in LDS (39.9 KB at N = 20): the KKT factor L, 1/D, the block
+//     inverses of the blocked substitution, the solve vector and the scaled matrix values; the
+//     primal/dual iterates, bounds and inverse scalings live in VGPRs (element i on lane i % 64,
+//     slot i / 64); a per-wave slab in global memory keeps the scalings D, E;
+//   * numeric factorization and both triangular solves are driven by host-compiled step
+//     schedules (symbolic.hpp): each step is a 64-lane pass of LDS reads, FMAs and LDS atomics;
+//   * wave reductions end with the gfx950 lane swaps (v_permlane16/32_swap), not readlanes;
 //   * arithmetic is fp64 throughout and follows OSQP 0.6's algorithm (Ruiz scaling, rho classes,
 //     ADMM with alpha relaxation, unscaled termination + infeasibility tests, adaptive rho).
 //
@@ -405,7 +407,7 @@ __device__ __forceinline__ void run_factor(const KParams& p, double* v, int lane
 enum : uint32_t { CT_INEQ = 0, CT_EQ = 1, CT_FREE = 2 };
 
 // Register-resident per-instance state.  Element i of an n- or m-vector lives on lane i % 64,
-// slot i / 64.  Scalings D, 1/D, E, 1/E live in the wave's scratch slab (read at checks only).
+// slot i / 64.  The scalings D, E live in the wave's scratch slab (read at checks only).
 template <int RN, int RM>
 struct Inst {
   double x[RN], q[RN];
@@ -1193,6 +1195,19 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   // immediate offset, so no second address register per slot
   constexpr int coff = 64 * (RN + RM);
   const uint32_t wcp = P.wcopy[lane], bcp = P.bcopy[lane];
+  // the copy-row selections as word masks in VGPRs (W start = value AND mask: the value or +0.0,
+  // bitwise the select it replaces).  Held as compare results they were SGPR pairs spilled to VGPR
+  // lanes, two readlanes per slot and pass in the loop (927k vs 925k solves/s)
+  uint32_t wmk[RN + RM], bmk[RN + RM];
+#pragma unroll
+  for (int r = 0; r < RN + RM; ++r) {
+    wmk[r] = 0u - ((wcp >> r) & 1u);
+    bmk[r] = 0u - ((bcp >> r) & 1u);
+    asm volatile("" : "+v"(wmk[r]), "+v"(bmk[r]));
+  }
+  auto and_d = [](double x, uint32_t mk) {
+    return __hiloint2double((int)((uint32_t)__double2hiint(x) & mk), (int)((uint32_t)__double2loint(x) & mk));
+  };
   // loop constants held in VGPRs (an opaque copy: otherwise they are re-read from the kernel
   // arguments inside the loop, with an lgkmcnt(0) wait that also drains the LDS queue)
   double sigma = p.s.sigma, alpha = p.s.alpha, alpha_c = 1.0 - p.s.alpha;
@@ -1219,20 +1234,19 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
     // The forward solve accumulates into W, which starts at 0 except on the copy rows
     // (Plan::wcopy: W_r = rhs_r, no solve task); the lanes' slots cover all of W
-    const uint32_t wcpi = wcp;  // per-slot lane masks hoisted (as bcpi below)
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       xp[r] = S.x[r];
       const double b = sigma * xp[r] - S.q[r];
       v[wsx[r] + coff] = b;
-      v[wsx[r]] = (wcpi >> r) & 1u ? b : 0.0;
+      v[wsx[r]] = and_d(b, wmk[r]);
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       zp[r] = S.z[r];
       bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
       v[wsz[r] + coff] = bz[r];
-      v[wsz[r]] = (wcpi >> (RN + r)) & 1u ? bz[r] : 0.0;
+      v[wsz[r]] = and_d(bz[r], wmk[RN + r]);
     }
     LDS_FENCE();
     T_END(T_VEC, t_v0);
@@ -1245,8 +1259,6 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     {
       // C = (1/D) W; W restarts at 0, or at C where the row's identity term is folded into it
       // (Plan::bcopy: the backward task has no MONE term)
-      const uint32_t bcpi = bcp;  // per-slot lane masks hoisted (an opaque per-iteration copy
-                                  // measured 0.3 % slower: its bit tests borrow record registers)
       double wv[RN + RM], dv[RN + RM];
 #pragma unroll
       for (int r = 0; r < RN + RM; ++r) {
@@ -1257,7 +1269,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       for (int r = 0; r < RN + RM; ++r) {  // C at the immediate distance coff: one ds_write2st64
         const double c = wv[r] * dv[r];
         v[P.W + lane + 64 * r + coff] = c;
-        v[P.W + lane + 64 * r] = (bcpi >> r) & 1u ? c : 0.0;
+        v[P.W + lane + 64 * r] = and_d(c, bmk[r]);
       }
     }
     LDS_FENCE();
