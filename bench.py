@@ -15,8 +15,10 @@ in the timed region).
 
 Rank 0 prints one JSON line: metric/value/... + roofline (graded on the LDS, the resource the
 solve steps run on; HBM and FP64 fractions beside it) + cold (single-shot) rate + cpu_baseline
-+ config3 (the N = 40 impulsive delta-v batch, BASELINE config 3, measured in the same run; see
-DESIGN.md, Measurement).  `value` counts the solves the engine ran: chasers that terminated
++ three legs measured in the same run, each with its own roofline: config3 (N = 40 impulsive
+delta-v, BASELINE config 3) and n40_accel (N = 40 continuous acceleration, the horizon of every
+reference script), both at the headline's window, and config4 (the continuous-time nonlinear loop,
+BASELINE config 4, --cont-steps sample periods).  `value` counts the solves the engine ran: chasers that terminated
 (reference src/trajectorySimulate.py:288-293) are skipped by the solver and not counted.
 """
 from __future__ import annotations
@@ -407,34 +409,53 @@ def bench_discrete(args, rank, world, device, dist):
     return out
 
 
-def bench_config3(args, rank, device):
-    """BASELINE config 3 in the same run: N = 40, impulsive delta-v input model (reference
-    src/trajectorySimulate.py:110-111), B = 65,536 chasers, the same warm closed loop, a shorter
-    timed window (its own figure, not the headline `value`)."""
+def lds_roof(iters_total, lds_iter, seconds, kernel_ms=None, fp64=None):
+    """LDS-graded roofline of a leg: the LDS bytes its solve launches moved (ADMM iterations x
+    lds_bytes_per_iter) over the leg's timed wall time."""
+    ach = iters_total * lds_iter / seconds / 1e9
+    out = {"bound": "lds", "achieved": ach, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+           "frac": ach / LDS_PEAK_GBS, "traffic": None, "kernel": "qp_batch_kernel",
+           "lds_bytes_per_iter": lds_iter, "admm_iters_timed": float(iters_total)}
+    if kernel_ms is not None:
+        out["kernel_ms_per_launch"] = kernel_ms
+    if fp64 is not None:
+        out["fp64"] = fp64
+    return out
+
+
+def bench_leg(args, rank, device, nx, dv):
+    """A discrete closed-loop leg in the same run, at the headline's window (args.steps timed
+    after args.warmup): N = 40 impulsive delta-v (BASELINE config 3, reference
+    src/trajectorySimulate.py:110-111) and N = 40 continuous acceleration (the horizon every
+    reference script runs: test/traj_eval_radial.py:57), B = 65,536 chasers each."""
     from mpc_arpo_project_amd import qp_model, scenarios
 
-    sim, mpc, fail, deb = scenarios.radial_scenario(Nx=40, isDeltaV=True)
+    sim, mpc, fail, deb = scenarios.radial_scenario(Nx=nx, isDeltaV=dv)
     prob = qp_model.build_problem(sim, mpc, fail, deb)
-    B, K, W, S = args.batch, args.config3_steps, 3, max(1, min(args.split, args.batch))
+    B, S = args.batch, max(1, min(args.split, args.batch))
+    K = args.leg_steps or args.steps
+    W = args.leg_warmup if args.leg_warmup is not None else args.warmup
     X0 = initial_states(B, 0, B, args.seed)
     run = closed_loop_run(prob, X0, B, K, W, S, args.eps, rank, device, None, track=None,
                           longest_first=args.order == "iters")
     it, act = run["it"], run["act"]
     roof = roofline(run, S, K, run["elapsed"])
-    attach_profiles(roof, B, 40, S, K, run["elapsed"])
+    attach_profiles(roof, B, nx, S, K, run["elapsed"])
     for c in run["cls"]:
         c.close()
-    return {"metric": f"MPC-QP solves/sec @ N=40, impulsive delta-v, CW, batch={B}; ADMM iters to "
+    model = "impulsive delta-v" if dv else "continuous acceleration"
+    return {"metric": f"MPC-QP solves/sec @ N={nx}, {model}, CW, batch={B}; ADMM iters to "
                       f"{args.eps:g}",
             "value": float(act.sum()) / run["elapsed"], "unit": "solves/s", "steps": K,
             "warmup": W, "ms_per_step": run["elapsed"] / K * 1e3,
-            "config": {"workload": f"warm closed-loop MPC-QP solves, radial CW scenario, N=Nx=40, "
-                                   f"Nc=Nb=5, impulsive delta-v (n={run['dims']['n']}, "
+            "config": {"workload": f"warm closed-loop MPC-QP solves, radial CW scenario, N=Nx={nx}, "
+                                   f"Nc=Nb=5, {model} (n={run['dims']['n']}, "
                                    f"m={run['dims']['m']})", "batch_per_gpu": B,
                        "streams_per_gpu": S},
             "roofline": {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac",
-                                              "kernel_ms_per_launch", "lds_bytes_per_iter",
-                                              "admm_iters_timed", "fp64")},
+                                              "traffic", "kernel", "kernel_ms_per_launch",
+                                              "lds_bytes_per_iter", "admm_iters_timed", "fp64")
+                         if k in roof},
             "admm_iters": {"mean": float(it[act].mean()), "median": float(np.median(it[act])),
                            "p90": float(np.percentile(it[act], 90)), "max": int(it[act].max())},
             "schedule": run["sched"]}
@@ -502,6 +523,13 @@ def bench_continuous(args, rank, world, device, dist):
         return None
     t_solve = np.array([e[0].elapsed_time(e[1]) for e in ev])
     t_rest = np.array([e[1].elapsed_time(e[2]) for e in ev])
+    lds_iter = lds_bytes_per_iter(sched["fwd_steps"], sched["bwd_steps"], dims["n"], dims["m"],
+                                  sched["atomics_per_step"])
+    it_timed = float(np.where(a, it, 0).sum())
+    # graded over the whole timed periods (plant + UKF + configure included); the solve launches
+    # alone beside it (their HIP-event time)
+    roof = lds_roof(it_timed, lds_iter, elapsed, kernel_ms=float(t_solve.mean()))
+    roof["frac_over_solve_launches"] = it_timed * lds_iter / (t_solve.sum() * 1e-3) / 1e9 / LDS_PEAK_GBS
     return {
         "metric": f"MPC-QP solves/sec @ N={nx} offset-free MPC in the continuous-time nonlinear "
                   f"loop (trajectorySimulateC), batch={B}; ADMM iters to {args.eps:g}",
@@ -515,6 +543,7 @@ def bench_continuous(args, rank, world, device, dist):
                                f"sub-steps at 1 ms (control held) + UKF + configure",
                    "batch_per_gpu": B, "global_batch": world * B, "N": nx,
                    "parallelism": f"shard{world}" if world > 1 else "single"},
+        "roofline": roof,
         "period_split_ms": {"solve": float(t_solve.mean()),
                             "plant_ukf_configure": float(t_rest.mean())},
         "admm_iters": {"mean": float(it[a].mean()) if a.any() else None,
@@ -538,9 +567,15 @@ def main(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle threads (default: every core in this process's affinity mask)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-config3", action="store_true",
-                    help="skip the N=40 delta-v (BASELINE config 3) figure of the default run")
-    ap.add_argument("--config3-steps", type=int, default=10)
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the N=40 legs (config 3 delta-v, N=40 continuous acceleration, "
+                         "config 4 continuous-time loop) of the default run")
+    ap.add_argument("--leg-steps", type=int, default=0,
+                    help="timed steps of the N=40 discrete legs (default: --steps)")
+    ap.add_argument("--leg-warmup", type=int, default=None,
+                    help="untimed steps of the N=40 discrete legs (default: --warmup)")
+    ap.add_argument("--cont-steps", type=int, default=5,
+                    help="timed sample periods of the config-4 leg of the default run")
     ap.add_argument("--continuous", action="store_true",
                     help="BASELINE config 4: the continuous-time nonlinear loop (default N=40)")
     ap.add_argument("--order", choices=("iters", "none"), default="none",
@@ -563,11 +598,18 @@ def main(argv=None):
     else:
         out = bench_discrete(args, rank, world, device, dist)
         default_cfg = (args.nx, args.dv) == (20, False)
-        if out is not None and world == 1 and default_cfg and not args.no_config3:
+        if out is not None and world == 1 and default_cfg and not args.no_legs:
+            for key, nx, dv in (("config3", 40, True), ("n40_accel", 40, False)):
+                try:
+                    out[key] = bench_leg(args, rank, device, nx, dv)
+                except Exception as e:  # report, never fake
+                    out[key] = {"error": repr(e)}
             try:
-                out["config3"] = bench_config3(args, rank, device)
+                ca = argparse.Namespace(**vars(args))
+                ca.nx, ca.dv, ca.steps, ca.warmup = 40, False, args.cont_steps, 1
+                out["config4"] = bench_continuous(ca, rank, world, device, dist)
             except Exception as e:  # report, never fake
-                out["config3"] = {"error": repr(e)}
+                out["config4"] = {"error": repr(e)}
     if out is not None:
         print(json.dumps(out), flush=True)
     if dist:

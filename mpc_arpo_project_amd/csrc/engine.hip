@@ -1503,7 +1503,6 @@ kernel_fn select_kernel(int n, int m, bool paired) {
   if (rn == 2) return pick<2, 4>(paired);
 #ifndef MPCQP_ONLY_SMALL
   if (rn == 4) return pick<4, 8>(paired);
-  if (rn == 8) return pick<8, 16>(paired);
 #endif
   return nullptr;
 }

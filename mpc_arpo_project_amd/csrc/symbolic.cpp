@@ -838,7 +838,8 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   {
     int rn = 0, rm = 0;
     if (!kernel_bucket(n, m, rn, rm)) {
-      pl.error = "problem too large for the engine's register-slot buckets";
+      pl.error = "problem too large for the engine's register-slot buckets (n <= 256, m <= 512, "
+                 "n + m < 768: the planar MPC up to Nx = 51)";
       return false;
     }
     pl.NKP = 64 * (rn + rm);

@@ -86,11 +86,14 @@ struct Ell {
 };
 
 // Register-slot bucket of the engine kernel: RN >= ceil(n / 64) slots for n-vectors, RM >= ceil(m /
-// 64) for m-vectors, from the instantiated set (2,4), (4,8), (8,16), with RN + RM > nk / 64 (a junk
-// slot).  false if no bucket fits.
+// 64) for m-vectors, from the instantiated set (2,4), (4,8), with RN + RM > nk / 64 (a junk slot).
+// false if no bucket fits: the reference's horizons (Nx 20-50) all fit (4,8) (up to
+// Nx = 51 for the planar model); an (8,16) build spilled 651 VGPRs (profiles/r03/
+// resource_usage.txt) and is not shipped, so larger problems are refused at create time.
+constexpr int KERNEL_MAX_RN = 4;
 inline bool kernel_bucket(int n, int m, int& rn, int& rm) {
   const int need_n = (n + 63) / 64, need_m = (m + 63) / 64, need_k = (n + m) / 64 + 1;
-  for (int b = 2; b <= 8; b *= 2)
+  for (int b = 2; b <= KERNEL_MAX_RN; b *= 2)
     if (need_n <= b && need_m <= 2 * b && 3 * b >= need_k) {
       rn = b, rm = 2 * b;
       return true;

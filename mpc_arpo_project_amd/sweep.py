@@ -5,16 +5,17 @@ The reference runs its experiments as serial Python loops of `trajectorySimulate
   * test/disturbRejComp.py:77-100                  noise lengths x MC runs, final distance
                                                    |x(i_term - 1) - xr| with / without rejection;
   * test/traj_eval_radial.py, traj_eval_in_track.py  the two approach geometries.
-(Every one of those runs re-seeds numpy with 123 at the top of trajectorySimulate,
-src/trajectorySimulate.py:28, so the reference's "Monte-Carlo" repetitions are identical runs;
-a sweep here gives every scenario its own noise stream instead.)
 
 A sweep is G = n_seeds x n_ics independent chasers; scenario g = s * n_ics + c runs initial
 condition c under noise stream g:
+  * defaults per approach are the reference scripts' own (SCENARIO_DEFAULTS): radial =
+    test/traj_eval_radial.py (Nx = 40, Noise((0.75, 0.75), 50), isReject, T_final = 150),
+    in-track = test/traj_eval_in_track.py (Nx = 40, noise None, no rejection, T_final = 100);
   * initial conditions: seeded samples inside the approach's line-of-sight cone, at rest
     (`initial_conditions`);
   * noise (when given): the device's counter-based Philox stream keyed by (noise_seed, g, draw),
-    so a scenario's result does not depend on how the sweep is sharded;
+    so a scenario's result does not depend on how the sweep is sharded (the reference has one
+    stream for every run, see below: a sweep over noise seeds needs a stream per scenario);
   * one process per GPU; rank r owns the contiguous ids [r G / W, (r + 1) G / W), split into
     `shards` closed loops on concurrent HIP streams; terminated chasers are skipped by the solver;
   * the only collective: after the run, one all-gather (RCCL over xGMI) of the per-scenario
@@ -26,8 +27,7 @@ condition c under noise stream g:
     python -m mpc_arpo_project_amd.sweep --scenario radial --seeds 1024 --ics 1024 --gpus 8
 
 The reference's two Monte-Carlo experiments, as sweep modes (one fixed initial condition,
-x0 = (100, 10, 0, 0), MC runs each with its own noise stream; rejecting and non-rejecting runs of
-one MC index share their noise stream, as the reference's seed-123 runs share theirs):
+x0 = (100, 10, 0, 0)):
 
     python -m mpc_arpo_project_amd.sweep --experiment disturb_rej [--mc 100]
         test/disturbRejComp.py:74-100: Nx = 40, T_final = 150, noise sigma 0.7, noise lengths
@@ -36,6 +36,16 @@ one MC index share their noise stream, as the reference's seed-123 runs share th
     python -m mpc_arpo_project_amd.sweep --experiment success_rates [--mc 300]
         test/saved_runs/success_rates_test.py:46-75: Nx = 40, T_final = 300, noise sigma 0.3
         held 50 samples, isReject = True; the count of isSuccess runs
+
+  --noise-stream reference (default): the reference's own noise.  trajectorySimulate re-seeds
+        numpy's global generator with 123 at every call (src/trajectorySimulate.py:28) and draws
+        noiseVec = sigMat @ normal(0, 1, 4) from it (:268, :352-356), so every Monte-Carlo run of
+        a setting is the SAME run: each setting's MC chasers get that one stream (host draws,
+        `reference_noise`), the outputs are the numbers the reference's scripts print (pinned by
+        tests/golden/exp_*.npz from the reference's own code) and `mc_runs_identical` checks the
+        repetitions came out equal;
+  --noise-stream independent: a variant the reference cannot produce -- every MC run its own
+        device stream (rejecting and non-rejecting runs of one MC index share theirs).
 """
 from __future__ import annotations
 
@@ -50,6 +60,23 @@ from . import launch, scenarios
 
 FIELDS = ("u0_x", "u0_y", "last_status", "admm_iters", "i_term", "success", "final_err",
           "n_fallback", "aborted")
+
+
+# the reference scripts' settings per approach (module docstring)
+SCENARIO_DEFAULTS = {
+    "radial": dict(nx=40, noise="0.75,0.75,50", reject=True, tfinal=150.0),     # traj_eval_radial.py:23-25,43,57,68
+    "in_track": dict(nx=40, noise="none", reject=False, tfinal=100.0),          # traj_eval_in_track.py:40-42,52,62
+}
+
+
+def reference_noise(sig, n_draws):
+    """the reference's noise draws 0..n_draws-1: numpy's global generator seeded with 123
+    (src/trajectorySimulate.py:28), noiseVec = sigMat @ random.normal(0, 1, 4) per draw (:268,
+    :352-356) with sigMat = diag(sig_x, sig_y, 0, 0) (src/mpcsim.py Noise.constructSigMat) ->
+    (n_draws, 4); draw k is the plant noise from step k * noise_length on"""
+    rs = np.random.RandomState(123)
+    sig_mat = np.diag([float(sig[0]), float(sig[1]), 0., 0.])
+    return np.array([sig_mat @ rs.normal(0, 1, 4) for _ in range(int(n_draws))])
 
 
 def initial_conditions(scenario: str, n_ics: int, seed: int = 20250328) -> np.ndarray:
@@ -93,9 +120,10 @@ def build(scenario: str, Nx: int, noise, isReject: bool, T_final: float):
 class Sweep:
     """The rank-local part of a sweep (device closed loops + run summaries)."""
 
-    def __init__(self, scenario="radial", n_seeds=1, n_ics=1024, Nx=20, noise=(0.3, 0.3, 50),
+    def __init__(self, scenario="radial", n_seeds=1, n_ics=1024, Nx=40, noise=(0.75, 0.75, 50),
                  isReject=True, T_final=150.0, rank=0, world=1, device="cuda", shards=2,
-                 ic_seed=20250328, noise_seed=123, eps=1e-3, keep_traj=False, x0=None):
+                 ic_seed=20250328, noise_seed=123, eps=1e-3, keep_traj=False, x0=None,
+                 noise_source=None):
         import torch
 
         from .closed_loop import ShardedClosedLoop
@@ -107,7 +135,8 @@ class Sweep:
         X = scenario_states(scenario, n_seeds, n_ics, self.lo, self.hi, ic_seed, x0)
         # the reference's default OSQP tolerances (eps_abs = eps_rel = 1e-3) unless asked otherwise
         self.loop = ShardedClosedLoop(self.prob, X, shards=shards, device=device, id_offset=self.lo,
-                                      noise=noise, noise_seed=noise_seed, eps_abs=eps, eps_rel=eps)
+                                      noise=noise, noise_seed=noise_seed, eps_abs=eps, eps_rel=eps,
+                                      noise_source=noise_source)
         self.loop.enable_tracking(self.nsim, *self.sim.suc_cond)
         self.traj = None
         if keep_traj:
@@ -172,8 +201,11 @@ def _timed_run(sw, dist, device):
     return time.perf_counter() - t0
 
 
-def experiment(name, mc, rank, world, device, dist, shards=2, eps=1e-3, noise_seed=123):
+def experiment(name, mc, rank, world, device, dist, shards=2, eps=1e-3, noise_seed=123,
+               noise_stream="reference"):
     """the reference's Monte-Carlo experiments (module docstring); returns rank 0's result dict"""
+    if noise_stream not in ("reference", "independent"):
+        raise ValueError(f"unknown noise stream {noise_stream!r}")
     if name == "disturb_rej":
         settings = [(L, rej) for L in NOISE_LENGTHS for rej in (False, True)]
         Nx, T_final, sig = 40, 150.0, 0.7
@@ -183,10 +215,19 @@ def experiment(name, mc, rank, world, device, dist, shards=2, eps=1e-3, noise_se
     else:
         raise ValueError(f"unknown experiment {name!r}")
     rows, secs, solves = [], 0.0, 0.0
+    nsim = int(T_final / 0.5)
     for L, rej in settings:
+        src = None
+        if noise_stream == "reference":
+            # one stream for every MC run (the reference re-seeds with 123 at every call)
+            w = reference_noise((sig, sig), nsim // int(L) + 1)
+
+            def src(k, w=w):
+                lo, hi = launch.shard_range(mc, rank, world)
+                return np.tile(w[min(k, len(w) - 1)], (hi - lo, 1))
         sw = Sweep("radial", mc, 1, Nx=Nx, noise=(sig, sig, int(L)), isReject=rej, T_final=T_final,
                    rank=rank, world=world, device=device, shards=shards, eps=eps,
-                   noise_seed=noise_seed, x0=X0_REF)
+                   noise_seed=noise_seed, x0=X0_REF, noise_source=src)
         el = _timed_run(sw, dist, device)
         S = launch.gather_rows(sw.summary(), sw.G, rank, world, dist)
         sw.close()
@@ -196,19 +237,26 @@ def experiment(name, mc, rank, world, device, dist, shards=2, eps=1e-3, noise_se
             rows.append(dict(noise_length=int(L), reject=rej, runs=int(Sn.shape[0]),
                              success=r["success"], aborted=r["aborted"],
                              final_err_mean=r["final_err_mean"], i_term_mean=r["i_term_mean"],
+                             mc_runs_identical=bool(np.all(Sn == Sn[:1])),
                              seconds=el))
             secs += el
             solves += float(Sn[:, FIELDS.index("i_term")].sum())
     if rank != 0:
         return None
     out = dict(experiment=name, n_gpus=world, mc=mc, nx=Nx, t_final=T_final, sigma=sig,
-               eps=eps, x0=list(X0_REF), seconds=secs, solves_per_s=solves / max(secs, 1e-9),
-               settings=rows)
+               eps=eps, x0=list(X0_REF), noise_stream=noise_stream, seconds=secs,
+               solves_per_s=solves / max(secs, 1e-9), settings=rows)
     if name == "disturb_rej":
-        # dist_ratios[i] = mean final distance with rejection / without (disturbRejComp.py:98-100)
+        # dist_ratios[i] = mean final distance with rejection / without (disturbRejComp.py:98-100);
+        # None where every run of a setting aborted (the reference's run would have raised)
         by = {(r["noise_length"], r["reject"]): r for r in rows}
-        out["dist_ratios"] = {int(L): by[(L, True)]["final_err_mean"] / by[(L, False)]["final_err_mean"]
-                              for L in NOISE_LENGTHS}
+
+        def ratio(L):
+            a, b = by[(L, True)]["final_err_mean"], by[(L, False)]["final_err_mean"]
+            return None if a is None or b is None or b == 0 else a / b
+        out["dist_ratios"] = {int(L): ratio(L) for L in NOISE_LENGTHS}
+        out["aborted"] = {int(L): by[(L, False)]["aborted"] + by[(L, True)]["aborted"]
+                          for L in NOISE_LENGTHS}
     else:
         out["success_count"] = rows[0]["success"]
         out["success_rate"] = rows[0]["success"] / rows[0]["runs"]
@@ -222,10 +270,12 @@ def main(argv=None):
     ap.add_argument("--seeds", type=int, default=1024)
     ap.add_argument("--ics", type=int, default=1024)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--nx", type=int, default=20)
-    ap.add_argument("--noise", default="0.3,0.3,50", help="sig_x,sig_y,noise_length or 'none'")
-    ap.add_argument("--no-reject", action="store_true")
-    ap.add_argument("--tfinal", type=float, default=150.0)
+    ap.add_argument("--nx", type=int, default=None, help="default: the scenario script's (40)")
+    ap.add_argument("--noise", default=None,
+                    help="sig_x,sig_y,noise_length or 'none' (default: the scenario script's)")
+    ap.add_argument("--reject", choices=("yes", "no"), default=None,
+                    help="offset-free disturbance rejection (default: the scenario script's)")
+    ap.add_argument("--tfinal", type=float, default=None)
     ap.add_argument("--eps", type=float, default=1e-3)
     ap.add_argument("--shards", type=int, default=2)
     ap.add_argument("--traj", action="store_true", help="gather trajectories to rank 0")
@@ -234,7 +284,15 @@ def main(argv=None):
                     help="the reference's Monte-Carlo experiment scripts (module docstring)")
     ap.add_argument("--mc", type=int, default=0,
                     help="Monte-Carlo runs per setting (default: the reference's 100 / 300)")
+    ap.add_argument("--noise-stream", choices=("reference", "independent"), default="reference",
+                    help="experiments: the reference's seed-123 stream for every run, or a "
+                         "stream per run (module docstring)")
     a = ap.parse_args(argv[1:])
+    dflt = SCENARIO_DEFAULTS[a.scenario]
+    a.nx = dflt["nx"] if a.nx is None else a.nx
+    a.noise = dflt["noise"] if a.noise is None else a.noise
+    a.tfinal = dflt["tfinal"] if a.tfinal is None else a.tfinal
+    a.no_reject = not dflt["reject"] if a.reject is None else a.reject == "no"
     if a.gpus > 1 and not launch.launched():
         return launch.relaunch(a.gpus, argv, module="mpc_arpo_project_amd.sweep")
     import torch
@@ -244,7 +302,8 @@ def main(argv=None):
         raise SystemExit(f"--gpus {a.gpus} but {world} ranks were launched")
     if a.experiment:
         mc = a.mc or (100 if a.experiment == "disturb_rej" else 300)
-        out = experiment(a.experiment, mc, rank, world, device, dist, shards=a.shards, eps=a.eps)
+        out = experiment(a.experiment, mc, rank, world, device, dist, shards=a.shards, eps=a.eps,
+                         noise_stream=a.noise_stream)
         if rank == 0:
             print(json.dumps(out), flush=True)
         if dist:

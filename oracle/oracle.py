@@ -95,6 +95,8 @@ def lib():
         L.oqp_set_state.restype = C.c_int
         L.oqp_batch_set_state.argtypes = [C.c_int, C.POINTER(C.c_void_p), dp, dp, dp, dp]
         L.oqp_batch_set_state.restype = C.c_int
+        L.oqp_set_jitter.argtypes = [vp, C.c_ulonglong]
+        L.oqp_set_jitter.restype = None
         _lib = L
     return _lib
 
@@ -165,6 +167,11 @@ class OracleOSQP:
         if not self._w:
             raise ValueError(f"oracle setup failed (code {err.value})")
         self.nnzA = int(self._Ap[-1])
+
+    def set_jitter(self, seed: int):
+        """parity-floor diagnostics: seed != 0 moves every KKT right-hand side entry by one ulp
+        (random direction, deterministic per seed) before each solve of the ADMM loop"""
+        lib().oqp_set_jitter(self._w, int(seed))
 
     def update(self, q=None, l=None, u=None, Px=None, Ax=None, Ax_idx=None):
         L = lib()

@@ -518,6 +518,8 @@ struct oqp_work {
   double *sol_x, *sol_y;
   int status, iter, status_polish, rho_updates;
   double obj_val, pri_res, dua_res;
+  /* parity-floor diagnostics only (oqp_set_jitter): xorshift state, 0 = off */
+  unsigned long long jitter;
 };
 
 /* scaling.c scale_data */
@@ -808,6 +810,17 @@ static void update_xz_tilde(oqp_work *w) {
   for (int i = 0; i < m; i++) w->xz_tilde[n + i] = w->z_prev[i] - w->rho_inv_vec[i] * w->y[i];
   /* qdldl_interface solve (non-polish): permute, solve, copy x~, z~ = b_z + rho^-1 nu */
   for (int k = 0; k < s->nk; k++) s->bp[k] = w->xz_tilde[s->perm[k]];
+  if (w->jitter) {
+    /* parity-floor diagnostics (oqp_set_jitter): every right-hand side entry moved by one ulp up
+     * or down -- a backward error of one ulp per KKT solve, the size of the difference between
+     * two valid summation orders of the triangular solves */
+    for (int k = 0; k < s->nk; k++) {
+      unsigned long long x = w->jitter;
+      x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+      w->jitter = x;
+      s->bp[k] = nextafter(s->bp[k], (x >> 63) ? INFINITY : -INFINITY);
+    }
+  }
   qdldl_solve(s->nk, s->Lp, s->Li, s->Lx, s->Dinv, s->bp);
   for (int i = 0; i < n; i++) w->xz_tilde[i] = s->bp[s->pinv[i]];
   for (int i = 0; i < m; i++) w->xz_tilde[n + i] += w->rho_inv_vec[i] * s->bp[s->pinv[n + i]];
@@ -1194,6 +1207,11 @@ int oqp_solve(oqp_work *w) {
 
 void oqp_get_x(const oqp_work *w, double *x) { memcpy(x, w->sol_x, sizeof(double) * (size_t)w->n); }
 void oqp_get_y(const oqp_work *w, double *y) { memcpy(y, w->sol_y, sizeof(double) * (size_t)w->m); }
+/* parity-floor diagnostics: seed != 0 turns on the one-ulp right-hand-side jitter of every KKT
+ * solve (update_xz_tilde), with a deterministic per-solver stream; 0 turns it off */
+void oqp_set_jitter(oqp_work *w, unsigned long long seed) {
+  w->jitter = seed ? seed * 0x9E3779B97F4A7C15ull | 1ull : 0ull;
+}
 int oqp_status(const oqp_work *w) { return w->status; }
 int oqp_iter(const oqp_work *w) { return w->iter; }
 int oqp_status_polish(const oqp_work *w) { return w->status_polish; }

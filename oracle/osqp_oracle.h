@@ -67,6 +67,10 @@ int oqp_update_rho(oqp_work *w, double rho);
 int oqp_warm_start(oqp_work *w, const double *x, const double *y);
 int oqp_solve(oqp_work *w);
 
+/* parity-floor diagnostics: seed != 0 moves every KKT right-hand side entry by one ulp (random
+ * direction, deterministic stream per solver) before each solve of the ADMM loop; 0 = off */
+void oqp_set_jitter(oqp_work *w, unsigned long long seed);
+
 /* results of the last solve */
 void oqp_get_x(const oqp_work *w, double *x);
 void oqp_get_y(const oqp_work *w, double *y);

@@ -105,6 +105,22 @@ def compare(a, b):
                 same_run=float(np.mean(same_run)))
 
 
-def ulp_perturbed(X0):
-    """every initial state coordinate moved by one ulp (towards +inf)"""
-    return np.nextafter(X0, np.inf)
+FLOOR_DRAWS = 4
+
+
+def ulp_perturbed(X0, draw=0):
+    """every initial state coordinate moved by one ulp: draw 0 towards +inf, draw 1 towards -inf,
+    later draws up or down at random (seeded by the draw) -- independent floor draws"""
+    if draw == 0:
+        return np.nextafter(X0, np.inf)
+    if draw == 1:
+        return np.nextafter(X0, -np.inf)
+    up = np.random.default_rng(1000 + draw).random(X0.shape) < 0.5
+    return np.where(up, np.nextafter(X0, np.inf), np.nextafter(X0, -np.inf))
+
+
+def floor_bound(floors, key, G):
+    """lower bound of an agreement figure from the floor's spread over its draws: the worst draw
+    less two standard deviations of the draws and one scenario"""
+    v = np.array([f[key] for f in floors])
+    return float(v.min() - 2 * v.std(ddof=1) - 1.0 / G)

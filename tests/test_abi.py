@@ -72,3 +72,22 @@ def test_invalid_structure_rejected():
         assert "upper" in str(e)
     else:
         raise AssertionError("lower-triangular P accepted")
+
+
+def test_horizon_limits():
+    """the reference's horizons (Nx 20-50) are planned; structures beyond the (4, 8)
+    register bucket (Nx > 51 for the planar model) are refused at analysis / create time instead
+    of running a spill-bound instantiation"""
+    from conftest import problem
+
+    for nx in (50, 51):
+        p = problem(nx, False)
+        _, _, _, st = _lib.analyze(triu_csc(p.P), p.A)
+        assert st["fwd_steps"] > 0
+    p = problem(52, False)
+    try:
+        _lib.analyze(triu_csc(p.P), p.A)
+    except _lib.MPCQPError as e:
+        assert "too large" in str(e)
+    else:
+        raise AssertionError("Nx = 52 accepted")

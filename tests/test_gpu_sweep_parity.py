@@ -1,10 +1,12 @@
 """Full-length sweeps, engine-driven vs oracle-driven (BASELINE config 5; tests/sweep_parity.py):
-256 chasers x 300 control steps each, the reference's run reduction (isSuccess, i_term, final
-distance; src/trajectorySimulate.py:359-387, test/disturbRejComp.py:88) compared chaser by
-chaser.  The closed loops are chaotic in the solver's rounding -- the oracle itself, restarted
-from initial states one ulp away, reproduces only ~70 % of its own runs exactly -- so the engine
-is held to that floor: its disagreement with the oracle may not exceed the oracle's disagreement
-with itself by more than a few scenarios (measured: profiles/r03/sweep_parity.json)."""
+256 chasers x the scenario's control steps each, the reference's run reduction (isSuccess,
+i_term, final distance; src/trajectorySimulate.py:359-387, test/disturbRejComp.py:88) compared
+chaser by chaser.  The closed loops are chaotic in the solver's rounding -- the oracle itself,
+restarted from initial states one ulp away, reproduces only ~70 % of its own runs exactly -- so
+the engine is held to that floor: four independent one-ulp draws of the oracle against itself
+give the floor's spread, and the engine's agreement with the oracle may not fall below the worst
+draw by more than two of the draws' standard deviations (sweep_parity.floor_bound; measured:
+profiles/r04/sweep_parity.json)."""
 import numpy as np
 import pytest
 
@@ -14,31 +16,36 @@ from mpc_arpo_project_amd import sweep
 pytestmark = pytest.mark.gpu
 
 CASES = [
-    # the sweep driver's default: radial, N = 20, noise (0.3, 0.3) held 50 samples, rejection on
-    ("radial", 20, (0.3, 0.3, 50), True),
-    # test/traj_eval_in_track.py: in-track, N = 40, no noise, no rejection
-    ("in_track", 40, None, False),
+    # test/traj_eval_radial.py: radial, N = 40, noise (0.75, 0.75) held 50 samples, rejection on,
+    # T_final = 150 (the sweep driver's radial default)
+    ("radial", 40, (0.75, 0.75, 50), True, 150.0),
+    # round 3's radial case: N = 20, noise (0.3, 0.3) held 50 samples, rejection on
+    ("radial", 20, (0.3, 0.3, 50), True, 150.0),
+    # test/traj_eval_in_track.py: in-track, N = 40, no noise, no rejection (T_final as round 3's)
+    ("in_track", 40, None, False, 150.0),
 ]
 
 
-@pytest.mark.parametrize("scenario,nx,noise,reject", CASES)
-def test_full_length_sweep_matches_oracle_driven_runs(scenario, nx, noise, reject):
-    sim, prob = sweep.build(scenario, nx, noise, reject, 150.0)
+@pytest.mark.parametrize("scenario,nx,noise,reject,tfinal", CASES)
+def test_full_length_sweep_matches_oracle_driven_runs(scenario, nx, noise, reject, tfinal):
+    sim, prob = sweep.build(scenario, nx, noise, reject, tfinal)
     nsim = int(sim.T_final / sim.time_stp)
     X0 = sweep.initial_conditions(scenario, 256)
     eng = spp.engine_run(prob, X0, nsim, sim.suc_cond, noise, 1e-3)
     orc = spp.oracle_run(prob, X0, nsim, sim.suc_cond, noise, 1e-3)
-    flo = spp.oracle_run(prob, spp.ulp_perturbed(X0), nsim, sim.suc_cond, noise, 1e-3)
-    ev, fl = spp.compare(eng, orc), spp.compare(flo, orc)
-    print(scenario, "engine vs oracle", ev, "oracle floor", fl)
+    floors = [spp.compare(spp.oracle_run(prob, spp.ulp_perturbed(X0, d), nsim, sim.suc_cond,
+                                         noise, 1e-3), orc) for d in range(spp.FLOOR_DRAWS)]
+    ev = spp.compare(eng, orc)
     G = ev["scenarios"]
-    # per-chaser agreement within a few scenarios of the oracle's own one-ulp floor
-    assert ev["same_run"] >= fl["same_run"] - 12 / G, (ev, fl)
-    assert ev["i_term_agree"] >= fl["i_term_agree"] - 12 / G, (ev, fl)
-    assert ev["success_agree"] >= fl["success_agree"] - 3 / G, (ev, fl)
+    print(scenario, nx, "engine vs oracle", ev)
+    for key in ("same_run", "i_term_agree", "success_agree"):
+        print(f"  {key}: engine {ev[key]:.4f}, floor draws "
+              f"{[round(f[key], 4) for f in floors]}, bound {spp.floor_bound(floors, key, G):.4f}")
+    # per-chaser agreement within the floor's spread
+    for key in ("same_run", "i_term_agree", "success_agree"):
+        assert ev[key] >= spp.floor_bound(floors, key, G), (key, ev, floors)
     # the statistics a sweep reports differ by no more than their own sampling noise: three
     # standard errors of the paired difference (bootstrap over the scenarios, sweep_parity.compare)
-    # -- the oracle against itself moved the median final error by 6.8 % on the radial case
     for key in ("success_rate", "i_term_mean", "final_err_median"):
         d = abs(ev[key][0] - ev[key][1])
         assert d <= 3 * ev["se"][key] + 1e-12, (key, d, ev["se"][key], ev)
