@@ -142,7 +142,9 @@ int mpcqp_set_skip(mpcqp_handle *h, const int32_t *skip);
  * unchanged (instances are independent); only the packing of the launch changes.  A closed loop
  * passes its chasers longest-first by the last solve's ADMM iterations, so the instances that run
  * to max_iter start first and the launch ends on short ones (no reference counterpart: OSQP solves
- * one problem at a time). */
+ * one problem at a time).  A non-permutation is undefined behaviour (a duplicate id races two
+ * waves on one instance's warm state, a missing id is never solved); the array may be rewritten
+ * between solves only on the handle's stream. */
 int mpcqp_set_order(mpcqp_handle *h, const int32_t *order);
 
 /* Copy the warm-start state the handle carries between solves (what OSQP keeps inside its

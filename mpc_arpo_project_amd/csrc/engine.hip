@@ -67,6 +67,7 @@ struct DevPlan {
   int MV, MVZ;  // resident scaled values [P | A] (CSC orders) and their zero slot
   const uint16_t *sra, *sca;  // lane-major row / column scaling slots (symbolic.hpp Plan::sra)
   int SJ;
+  int XCH, XID;  // two-wave kernel: exchange slots and the handed-over instance id (Plan::XCH)
 };
 
 struct KParams {
@@ -1054,8 +1055,9 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
   LDS_FENCE();
 }
 
-// end of scale_data: constraint classes, scaled bounds, D / E and the scaled matrices parked in
-// the per-wave slab (and their ELL copies for the residual mat-vecs)
+// end of scale_data: constraint classes, scaled bounds, D / E into the per-wave slab, and the
+// scaled values [P | A] copied from the scaling overlay into the resident MV region of the image
+// (read from there by the residual mat-vecs, certificates, KKT (re)assembly and the objective)
 template <int RN, int RM>
 __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs, Inst<RN, RM>& S,
                                              const Slab& sb, double* v, int lane, const double (&D)[RN],
@@ -1449,6 +1451,16 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
   if ((uint32_t)(uintptr_t)lds != 0u) __builtin_trap();  // schedule byte addresses assume base 0
   double* v = lds;
   double* scr = p.scratch + (size_t)blockIdx.x * slab_doubles(p.pl);
+#ifdef MPCQP_PAD_AGPR
+  // diagnostic builds only (the > 190-AGPR shard-overlap cliff): MPCQP_PAD_AGPR extra
+  // accumulation registers held live across the whole kernel, nothing else changed
+  uint32_t pad[MPCQP_PAD_AGPR];
+#pragma unroll
+  for (int k = 0; k < MPCQP_PAD_AGPR; ++k) {
+    pad[k] = (uint32_t)k * 2654435761u + (uint32_t)threadIdx.x;
+    asm volatile("" : "+a"(pad[k]));
+  }
+#endif
   for (;;) {
     unsigned int inst = 0;
     if (lane == 0) inst = atomicAdd(p.counter, 1u);
@@ -1467,7 +1479,18 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
     solve_instance<RN, RM, PAIRED>(p, (int)inst, v, scr, ilane);
     LDS_FENCE();
   }
+#ifdef MPCQP_PAD_AGPR
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < MPCQP_PAD_AGPR; ++k) {
+    asm volatile("" : "+a"(pad[k]));
+    acc ^= pad[k];
+  }
+  if (acc == 0x12345678u && p.timing) p.timing[0] = acc;  // keeps the pad live; never true in practice
+#endif
 }
+
+#include "engine_pair.inc"
 
 // ---------------------------------------------------------------------------------------- host
 thread_local std::string g_err;
@@ -1492,20 +1515,26 @@ int cap_m() { return env_int("MPCQP_CAPM", 0); }  // 0: chosen per structure
 int cap_w() { return env_int("MPCQP_CAPW", 0); }
 
 template <int RN, int RM>
-kernel_fn pick(bool paired) {
+kernel_fn pick(bool paired, int waves) {
+  if (waves == 2)
+    return paired ? qp_pair_kernel<RN / 2, RM / 2, true> : qp_pair_kernel<RN / 2, RM / 2, false>;
   return paired ? qp_batch_kernel<RN, RM, true> : qp_batch_kernel<RN, RM, false>;
 }
 
 // RN = ceil(n/64) and RM = ceil(m/64) rounded up to the instantiated buckets; the plan's step kind
-kernel_fn select_kernel(int n, int m, bool paired) {
+// and waves per instance
+kernel_fn select_kernel(int n, int m, bool paired, int waves) {
   int rn = 0, rm = 0;
   if (!kernel_bucket(n, m, rn, rm)) return nullptr;
-  if (rn == 2) return pick<2, 4>(paired);
+  if (rn == 2) return pick<2, 4>(paired, waves);
 #ifndef MPCQP_ONLY_SMALL
-  if (rn == 4) return pick<4, 8>(paired);
+  if (rn == 4) return pick<4, 8>(paired, waves);
 #endif
   return nullptr;
 }
+
+// waves per instance of the solve kernel (MPCQP_WAVES: 1 or 2; DESIGN.md, Two waves per instance)
+int waves_per_instance() { return env_int("MPCQP_WAVES", 1) == 2 ? 2 : 1; }
 
 template <typename T>
 size_t push_blob(std::vector<char>& blob, const std::vector<T>& v) {
@@ -1534,6 +1563,7 @@ struct mpcqp_handle {
   const int32_t* skip = nullptr;   // mpcqp_set_skip
   const int32_t* order = nullptr;  // mpcqp_set_order
   int grid = 0, lds_bytes = 0, waves_per_cu = 0;
+  int block = 64;  // threads per workgroup: 64 per wave of an instance
   kernel_fn kern = nullptr;
 };
 
@@ -1597,11 +1627,14 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   h->set = *s;
   h->B = batch;
   h->stream = (hipStream_t)stream;
-  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, h->plan, cap_m(), cap_w())) {
+  const int waves = waves_per_instance();
+  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, h->plan, cap_m(), cap_w(),
+                        163840, 4, waves)) {
     std::string e = h->plan.error;
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, e);
   }
+  h->block = 64 * h->plan.waves;
   const Plan& pl = h->plan;
   if (pl.CACC - pl.W != pl.NKP) {  // the kernel addresses C as W + NKP (an immediate offset)
     delete h;
@@ -1616,7 +1649,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     return fail(code, msg);
   };
   {
-    h->kern = select_kernel(pl.n, pl.m, pl.paired);
+    h->kern = select_kernel(pl.n, pl.m, pl.paired, pl.waves);
     if (!h->kern) {
       delete h;
       return fail(MPCQP_E_UNSUPPORTED, "problem dimensions exceed the instantiated kernels");
@@ -1687,6 +1720,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.S_ZERO = pl.S_ZERO;
     dp.MV = pl.MV, dp.MVZ = pl.MVZ;
     dp.sra = (const uint16_t*)(b + o_sra), dp.sca = (const uint16_t*)(b + o_sca), dp.SJ = pl.SJ;
+    dp.XCH = pl.XCH, dp.XID = pl.XID;
     // the vector passes address C through W's slot plus the compile-time distance 64 (RN + RM)
     if (pl.CACC - pl.W != pl.NKP || pl.NKP != 64 * (pl.RN + pl.RM))
       return cleanup_fail(MPCQP_E_INVALID, "internal: C region not at the kernel's distance from W");
@@ -1708,10 +1742,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
                             lds_cap) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipFuncSetAttribute");
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, 64, lds_alloc) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, h->block, lds_alloc) !=
             hipSuccess || nb <= 0)
       return cleanup_fail(MPCQP_E_UNSUPPORTED, "kernel does not fit on a CU (LDS/VGPR)");
-    h->waves_per_cu = nb;
+    h->waves_per_cu = nb * pl.waves;
     h->lds_bytes = lds_alloc;
     h->grid = std::min(batch, nb * ncu);
   }
@@ -1820,7 +1854,7 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   p.skip = h->skip;
   p.order = h->order;
   HIPCHK(hipMemsetAsync(h->counter, 0, 64, h->stream));
-  hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(64), h->lds_bytes, h->stream, p);
+  hipLaunchKernelGGL(h->kern, dim3(h->grid), dim3(h->block), h->lds_bytes, h->stream, p);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1936,7 +1970,8 @@ int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t
                   int32_t* nnzL, int32_t* stats) {
   if (!st || !nnzL) return fail(MPCQP_E_INVALID, "null argument");
   Plan pl;
-  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w()))
+  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w(), 163840,
+                        4, waves_per_instance()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   const int cap = *nnzL;
   *nnzL = pl.nnzL;
@@ -1958,8 +1993,9 @@ int mpcqp_schedule_check(const mpcqp_structure* st, const double* Px, const doub
                          double sigma, const double* rho_vec, const double* rhs, double* sol,
                          int64_t* model) {
   if (!st || !Px || !Ax || !rho_vec || !rhs || !sol) return fail(MPCQP_E_INVALID, "null argument");
-  Plan pl;
-  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w()))
+  Plan pl;  // the plan mpcqp_create would build (MPCQP_WAVES included)
+  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w(), 163840,
+                        4, waves_per_instance()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   if (model) {
     const LdsModel md = model_lds(pl);

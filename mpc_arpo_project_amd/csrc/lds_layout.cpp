@@ -253,6 +253,8 @@ struct Opt {
         const int p1 = used[rng.below((int)used.size())];
         int p2 = rng.below(256);
         if (p2 == p1) continue;
+        // two waves per instance: a segment stays in its wave's half (positions 0 + 1 / 2 + 3)
+        if (pl.waves == 2 && (p1 / 128) != (p2 / 128)) continue;
         std::swap(s[p1], s[p2]);
         const bool ok = lane_ok(p1 % 64) && lane_ok(p2 % 64);
         std::swap(s[p1], s[p2]);

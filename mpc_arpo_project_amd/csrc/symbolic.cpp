@@ -173,8 +173,56 @@ int pack_solve_level_free(const std::vector<Task>& tasks, const Plan& pl, std::v
     }
   const uint32_t zb = (uint32_t)pl.ZERO * 8u;
   int nsteps = 0;
-  for (size_t s0 = 0; s0 < segs.size();) {
-    const size_t s1 = std::min(segs.size(), s0 + 256);
+  // two waves per instance: each step's segments split into the half of positions 0 + 1 (wave 0)
+  // and the half of positions 2 + 3 (wave 1), every target's segments of a step in one half --
+  // a target is assigned whole to the half with room (fullest-first), consecutive steps take the
+  // rest.  half[] per segment: 0 / 1 (only the positions of that half are offered to it)
+  std::vector<int> half(segs.size(), -1);
+  std::vector<size_t> cut;  // step boundaries over segs (two-wave split only)
+  if (pl.waves == 2) {
+    // tasks by segment count, largest first (a better two-way partition of each step)
+    {
+      std::vector<std::pair<size_t, size_t>> runs;  // (begin, end) of each task's segments
+      for (size_t a = 0; a < segs.size();) {
+        size_t b = a;
+        while (b < segs.size() && segs[b].target == segs[a].target) ++b;
+        runs.push_back({a, b});
+        a = b;
+      }
+      std::stable_sort(runs.begin(), runs.end(), [](const std::pair<size_t, size_t>& x,
+                                                    const std::pair<size_t, size_t>& y) {
+        return x.second - x.first > y.second - y.first;
+      });
+      std::vector<Seg> sorted;
+      for (auto& r : runs) sorted.insert(sorted.end(), segs.begin() + r.first, segs.begin() + r.second);
+      segs.swap(sorted);
+    }
+    std::vector<Seg> out;
+    std::vector<int> oh;
+    size_t i = 0;
+    while (i < segs.size()) {
+      int room[2] = {128, 128};
+      const size_t st0 = out.size();
+      while (i < segs.size()) {
+        size_t j = i;
+        while (j < segs.size() && segs[j].target == segs[i].target) ++j;  // one task's segments
+        const int cnt = (int)(j - i);
+        int h = room[0] >= room[1] ? 0 : 1;
+        if (room[h] < cnt && room[1 - h] >= cnt) h = 1 - h;
+        const int take = std::min(cnt, room[h]);
+        if (take == 0) break;
+        for (int k = 0; k < take; ++k) out.push_back(segs[i + k]), oh.push_back(h);
+        room[h] -= take;
+        i += take;
+        if (take < cnt) break;  // the rest of this task goes to the next step
+      }
+      cut.push_back(out.size() - st0);
+    }
+    segs.swap(out);
+    half.swap(oh);
+  }
+  for (size_t s0 = 0, ci = 0; s0 < segs.size(); ++ci) {
+    const size_t s1 = pl.waves == 2 ? s0 + cut[ci] : std::min(segs.size(), s0 + 256);
     const size_t base = tbl.size();
     tbl.resize(base + SOLVE_STEP_WORDS, zb);
     uint32_t* terms = tbl.data() + base;
@@ -199,6 +247,7 @@ int pack_solve_level_free(const std::vector<Task>& tasks, const Plan& pl, std::v
       for (int pos = 0; pos < 256; ++pos) {
         if (used[pos]) continue;
         const int l = pos / 4, q = pos % 4, h = l / 32, grp = l / 16;
+        if (half[s] >= 0 && q / 2 != half[s]) continue;  // two waves: this segment's half only
         int pen = 4 * at[(q * 4 + grp) * 16 + g.target % 16];
         pen += rd_pen(2 * q, h, g.b0) + rd_pen(2 * q + 1, h, g.b1);
         if (pen < bestp) bestp = pen, best = pos;
@@ -264,7 +313,49 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
     // this step's units: pairs (two segments of one target, lane positions 0 + 1) first, most
     // segments first; then single segments into positions 2 / 3, then into free pair positions
     std::vector<std::vector<Seg>> units;
-    {
+    // two waves per instance (Plan::waves == 2): wave 0 executes the pair positions (one atomic
+    // per lane), wave 1 the single positions 2 / 3; every target of the step goes whole to one
+    // half: a target with two or more segments to the pairs while lanes are free (a half pair for
+    // an odd count), otherwise to the singles; what does not fit waits for the next step.
+    // unit_half[u]: 0 pair lane (one or two segments), 1 single position
+    std::vector<int> unit_half;
+    if (pl.waves == 2) {
+      std::vector<int> ord(rem.size());
+      for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+      std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return rem[x].size() > rem[y].size(); });
+      int roomA = 64, roomB = 128;
+      auto takeA = [&](int i, int nseg) {
+        for (int k = 0; k < nseg; k += 2) {
+          if (k + 1 < nseg)
+            units.push_back({rem[i][k], rem[i][k + 1]});
+          else
+            units.push_back({rem[i][k]});
+          unit_half.push_back(0);
+          roomA--;
+        }
+        rem[i].erase(rem[i].begin(), rem[i].begin() + nseg);
+      };
+      auto takeB = [&](int i, int nseg) {
+        for (int k = 0; k < nseg; ++k) units.push_back({rem[i][k]}), unit_half.push_back(1);
+        roomB -= nseg;
+        rem[i].erase(rem[i].begin(), rem[i].begin() + nseg);
+      };
+      for (int i : ord) {
+        const int sz = (int)rem[i].size();
+        if (sz == 0) continue;
+        const int lanes = (sz + 1) / 2;
+        if (sz >= 2 && lanes <= roomA)
+          takeA(i, sz);
+        else if (sz <= roomB)
+          takeB(i, sz);
+        else if (sz >= 2 && roomA > 0)
+          takeA(i, std::min(sz, 2 * roomA));
+        else if (roomB > 0)
+          takeB(i, std::min(sz, roomB));
+        else if (roomA > 0)
+          takeA(i, std::min(sz, 2 * roomA));
+      }
+    } else {
       std::vector<int> ord(rem.size());
       for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
       std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return rem[x].size() > rem[y].size(); });
@@ -285,6 +376,7 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
             pairs--;
         }
     }
+    if (pl.waves != 2) unit_half.assign(units.size(), -1);
     // placement: the free position whose operands and target collide least with those placed
     // (ds_read_b64: two 32-lane halves, bank = slot mod 32, broadcast; ds_add_f64: four 16-lane
     // groups, bank = slot mod 16) -- the layout optimiser refines it
@@ -314,11 +406,27 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
       tg[l * 4 + q] = (uint32_t)g.target * 8u;
     };
     int npairs = 0;
-    for (const auto& u : units) npairs += u.size() == 2;
+    for (size_t ui = 0; ui < units.size(); ++ui) npairs += units[ui].size() == 2 || unit_half[ui] == 0;
     int placed_pairs = 0;
-    for (const auto& u : units) {
+    for (size_t ui = 0; ui < units.size(); ++ui) {
+      const auto& u = units[ui];
       const Seg& g = u[0];
       int best = -1, bestp = 1 << 30;
+      if (unit_half[ui] == 0 && u.size() == 1) {  // two waves: a half pair (segment 1 unused)
+        for (int l = 0; l < 64; ++l) {
+          if (used[l]) continue;
+          const int h = l / 32;
+          int pen = 4 * at[(0 * 4 + l / 16) * 16 + g.target % 16];
+          pen += rd_pen(0, h, g.b0) + rd_pen(1, h, g.b1);
+          if (pen < bestp) bestp = pen, best = l;
+          if (pen == 0) break;
+        }
+        put(0, best, g);
+        used[64 + best] = 1;  // segment 1 of this lane stays unused
+        at[(0 * 4 + best / 16) * 16 + g.target % 16]++;
+        placed_pairs++;
+        continue;
+      }
       if (u.size() == 2) {
         for (int l = 0; l < 64; ++l) {
           if (used[l]) continue;
@@ -338,7 +446,8 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
       // when those are full, and never one a later pair needs
       int free_pairs = 0;
       for (int l = 0; l < 64; ++l) free_pairs += !used[l];
-      const bool pair_ok = free_pairs > npairs - placed_pairs;
+      // two waves: a single of the singles half never takes a pair position
+      const bool pair_ok = free_pairs > npairs - placed_pairs && unit_half[ui] != 1;
       for (int pass = 0; pass < 2 && best < 0; ++pass)
         for (int pos = 0; pos < 256; ++pos) {
           const int q = pos / 64, l = pos % 64;
@@ -654,9 +763,10 @@ std::vector<std::vector<Task>> place_accumulations(std::vector<std::vector<Task>
 }
 
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, Plan& pl, int capM, int capW, bool paired) {
+                const int32_t* Ai, Plan& pl, int capM, int capW, bool paired, int waves) {
   pl = Plan();
   pl.paired = paired;
+  pl.waves = waves == 2 ? 2 : 1;
   pl.n = n, pl.m = m, pl.nk = n + m;
   const int nk = n + m;
   pl.nnzP = Pp[n];
@@ -1239,39 +1349,18 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     pl.error = "problem too large for the residual layout";
     return false;
   }
-  auto positions = [](const Ell& e, int base, int cnt, std::vector<uint16_t>& pos) {
-    pos.assign(cnt, 0xffff);
-    for (size_t t = 0; t < e.src.size(); ++t) {
-      const int k = (int)e.src[t] - base;
-      if (e.src[t] != 0xffff && k >= 0 && k < cnt && pos[k] == 0xffff) pos[k] = (uint16_t)t;
-    }
-    for (uint16_t x : pos)
-      if (x == 0xffff) return false;
-    return true;
-  };
-  if (!positions(pl.ellA, pl.S_A, pl.nnzA, pl.posA) || !positions(pl.ellP, pl.S_P, pl.nnzP, pl.posP) ||
-      pl.ellA.src.size() >= 65535 || pl.ellP.src.size() >= 65535) {
-    pl.error = "residual layout does not cover every matrix entry";
+  if (pl.ellA.src.size() >= 65535 || pl.ellP.src.size() >= 65535) {
+    pl.error = "residual layout too large for 16-bit indices";
     return false;
   }
-  // ---- scaling index overlay behind the scaling value overlay (grows the image only if needed)
+  // ---- the Ruiz rescale's operand slots of the value overlay [P | A] (row and column scaling),
+  // lane-major for the kernel's registers (Plan::sra / sca)
   {
-    auto& b = pl.sci_block;
-    b.clear();
-    auto put = [&](const std::vector<uint16_t>& v, int cnt, int& off) {
-      off = (int)b.size();
-      b.insert(b.end(), v.begin(), v.begin() + cnt);
-    };
-    put(pl.ellP.src, pl.ellP.total, pl.sci_eP);
-    put(pl.ellAt.src, pl.ellAt.total, pl.sci_eAt);
-    put(pl.ellA.src, pl.ellA.total, pl.sci_eA);
     std::vector<uint16_t> ra, ca;
     for (int k = 0; k < pl.nnzP; ++k)
       ra.push_back((uint16_t)(pl.S_DT + pl.Pi[k])), ca.push_back((uint16_t)(pl.S_DT + pl.Pcol[k]));
     for (int k = 0; k < pl.nnzA; ++k)
       ra.push_back((uint16_t)(pl.S_ET + pl.Ai[k])), ca.push_back((uint16_t)(pl.S_DT + pl.Acol[k]));
-    put(ra, (int)ra.size(), pl.sci_ra);
-    put(ca, (int)ca.size(), pl.sci_ca);
     const int cnt = (int)ra.size();
     pl.SJ = ((cnt + 63) / 64 + 3) / 4 * 4;
     pl.sra.assign((size_t)64 * pl.SJ, 0);
@@ -1282,17 +1371,20 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
         pl.sra[(size_t)l * pl.SJ + j] = k < cnt ? ra[k] : 0;
         pl.sca[(size_t)l * pl.SJ + j] = k < cnt ? ca[k] : 0;
       }
-    while (b.size() % 8) b.push_back(0);
-    // ELL padding reads a zero double kept behind the value overlay (no conditional LDS reads)
+    // ELL padding of the Ruiz column / row norms reads a zero double kept behind the value
+    // overlay (no conditional LDS reads)
     pl.S_ZERO = pl.S_ET + m;
-    for (int k = 0; k < pl.sci_ra; ++k)
-      if (b[k] == 0xffff) b[k] = (uint16_t)pl.S_ZERO;
     if (pl.S_ZERO + 1 > pl.LDS_N) pl.LDS_N = (pl.S_ZERO + 2) & ~1;
   }
   // ---- resident scaled values (Plan::MV) behind the image; the ELL terms' LDS value slots
   pl.MV = (pl.LDS_N + 1) & ~1;
   pl.MVZ = pl.MV + pl.nnzP + pl.nnzA;
   pl.LDS_N = (pl.MVZ + 2) & ~1;
+  if (pl.waves == 2) {  // the two-wave kernel's exchange slots and the handed-over instance id
+    pl.XCH = pl.LDS_N;
+    pl.XID = pl.XCH + XCH_DOUBLES;
+    pl.LDS_N = (pl.XID + 2) & ~1;
+  }
   if (pl.LDS_N * 8 > (int)META_TGT_MASK || pl.LDS_N >= 65535) {
     pl.error = "LDS image too large for the resident matrix values";
     return false;
@@ -1338,12 +1430,12 @@ void finish_copy_masks(Plan& pl) {
 
 bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                       const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu,
-                      int max_per_cu) {
+                      int max_per_cu, int waves) {
   // the LDS layout optimiser runs on the chosen plan (MPCQP_NO_ANNEAL=1: off, diagnostics)
   const bool anneal = !getenv("MPCQP_NO_ANNEAL") && !getenv("MPCQP_NO_LAYOUT");
   const char* fp = getenv("MPCQP_PAIRED");  // diagnostics: force the step kind
   if (capM > 0 && capW > 0) {
-    if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW, !fp || atoi(fp) != 0)) return false;
+    if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW, !fp || atoi(fp) != 0, waves)) return false;
     if (anneal) optimize_lds(plan);
     finish_copy_masks(plan);
     return true;
@@ -1352,6 +1444,7 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
   // structure key
   std::vector<int32_t> key;
   key.push_back(n), key.push_back(m), key.push_back(lds_per_cu), key.push_back(max_per_cu);
+  key.push_back(waves);
   key.push_back(anneal);
   key.push_back(fp ? atoi(fp) : -1);
   const char* cm = getenv("MPCQP_COPY_ROWS");  // diagnostics: the copy-row mode (build_plan)
@@ -1386,7 +1479,7 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
     for (int cm : CM)
       for (int cw : CW) {
         Plan pl;
-        if (!build_plan(n, m, Pp, Pi, Ap, Ai, pl, cm, cw, pk != 0)) continue;
+        if (!build_plan(n, m, Pp, Pi, Ap, Ai, pl, cm, cw, pk != 0, waves)) continue;
         const int lds = ((pl.LDS_N + 1) & ~1) * 8;
         const int per_cu = std::min(max_per_cu, lds_per_cu / std::max(lds, 1));
         const int cost = (pl.nfwd + pl.nbwd) * (pk ? 92 : 100);
@@ -1400,7 +1493,7 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
   }
   if (!found) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);  // reports the error
   if (getenv("MPCQP_DUMP_CAPS")) fprintf(stderr, "caps %d %d paired %d\n", bm, bw, (int)bp);
-  if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw, bp)) return false;
+  if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw, bp, waves)) return false;
   if (anneal) optimize_lds(plan);
   finish_copy_masks(plan);
   {

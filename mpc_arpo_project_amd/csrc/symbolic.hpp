@@ -45,6 +45,9 @@ constexpr int SOLVE_STEP_WORDS = SOLVE_TERM_WORDS + 64 * 4;
 // half uses), ONE, MONE, padding
 constexpr int ZERO_BLOCK = 32;
 constexpr int CONST_SLOTS = ZERO_BLOCK + 4;
+// cross-wave exchange of the two-wave kernel: values per wave and buffer
+constexpr int XCH_K = 8;
+constexpr int XCH_DOUBLES = 2 * 2 * XCH_K;
 
 // meta word: per-lane fields, then the step-wide C and glog (identical in every lane)
 constexpr uint32_t META_TGT_MASK = 0x1ffffu;  // factorization: LDS byte address of the target
@@ -128,23 +131,18 @@ struct Plan {
   int nN = 0, nG = 0, nGP = 0;
   // scaling-phase overlay of the same LDS: scaled P, scaled A, D_temp, E_temp
   int S_P = 0, S_A = 0, S_DT = 0, S_ET = 0;
-  // scaling index overlay (LDS, u16 units from the image base, 16-byte aligned): the ELL src
-  // lists of P, A', A and the (row, column) of every P and A entry, copied in once per solve so
-  // the Ruiz passes read indices from LDS; offsets relative to SCI
-  int SCI = 0, S_ZERO = 0;  // S_ZERO: a zero double (in doubles) for the ELL padding
+  // S_ZERO: a zero double (in doubles) behind the value overlay, read by the ELL padding of the
+  // Ruiz column / row norms
+  int S_ZERO = 0;
   // resident scaled matrix values [P (upper CSC) | A (CSC)] behind everything else of the image:
   // written at the end of the Ruiz scaling, read by the residual mat-vecs, the infeasibility
   // certificates, every (re)assembly of the KKT values and the objective; MVZ holds a zero
   int MV = 0, MVZ = 0;
-  int sci_eP = 0, sci_eAt = 0, sci_eA = 0;
-  // the Ruiz rescale's operand slots of the value overlay [P | A] (CSC orders): row scaling slot
-  // (S_DT + i for P, S_ET + i for A) and column scaling slot (S_DT + j)
-  int sci_ra = 0, sci_ca = 0;
-  // the same row / column scaling slots lane-major: value k = 64 j + l of [P | A] at [l][j],
-  // j < SJ (a multiple of 4; padding -> S_ZERO), held in registers by the Ruiz passes
+  // the Ruiz rescale's row / column scaling slots of every value k = 64 j + l of [P | A] (CSC
+  // orders; S_DT + i for P's rows, S_ET + i for A's, S_DT + j for columns) lane-major at [l][j],
+  // j < SJ (a multiple of 4; padding -> 0), held in registers by the Ruiz passes
   int SJ = 0;
   std::vector<uint16_t> sra, sca;
-  std::vector<uint16_t> sci_block;  // padded to a multiple of 8 entries
   // KKT assembly: LDS slot of each P entry (diagonal -> D slot), A entry, rho diagonal,
   // sigma diagonal (D slot of x_j)
   std::vector<uint16_t> slotP, slotA, slotRho, slotSig;
@@ -161,6 +159,13 @@ struct Plan {
   std::vector<uint32_t> bcopy;
   std::vector<uint8_t> bcopy_row;
   bool paired = true;  // solve-step kind (build_plan)
+  // waves per instance the solve steps are laid out for (build_plan): 1, or 2 -- wave 0 executes
+  // segment positions 0 + 1 of every lane, wave 1 positions 2 + 3; within a step every target's
+  // segments sit in one of the two halves, so each target is summed by one wave in a fixed order
+  int waves = 1;
+  // two-wave kernel: LDS slots (doubles) of the cross-wave exchange (XCH_DOUBLES: two buffers x two
+  // waves x XCH_K values) and of the instance id the first wave hands the second (XID)
+  int XCH = 0, XID = 0;
   // schedules (STEP_WORDS words per step): factorization of U = L D and D by levels, then
   // (after the flat pass L = U * (1/D)_col) the block-inverse tail; forward and backward solves
   std::vector<uint32_t> fac, tail, fwd, bwd;
@@ -174,9 +179,6 @@ struct Plan {
   std::vector<uint16_t> Psp, Psk, Pso; // symmetric traversal: per column j the P entries of
                                        // column j and row j, their position and the other index
   Ell ellA, ellAt, ellP;  // A x (rows of A), A' y (columns), P x (symmetric rows of P)
-  // position of every A entry (CSC order) in ellA's value list and of every P entry (upper CSC) in
-  // ellP's: the per-instance scaled values live only in the ELL copies
-  std::vector<uint16_t> posA, posP;
   int levels_fwd = 0, levels_bwd = 0;
   std::vector<int> fwd_level_steps, bwd_level_steps;  // solve steps of each level (diagnostics)
   std::string error;
@@ -191,7 +193,8 @@ void finish_copy_masks(Plan& plan);
 // paired: solve steps with segments 0 + 1 of a lane on one target (three atomics per lane and
 // step, SOLVE_TERM_WORDS above) or with four independent segments (four atomics).
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, Plan& plan, int capM = 128, int capW = 384, bool paired = true);
+                const int32_t* Ai, Plan& plan, int capM = 128, int capW = 384, bool paired = true,
+                int waves = 1);
 
 // build_plan with the block caps and the step kind chosen per structure: over a grid of (capM <=
 // 192, capW) x {paired, unpaired}, the plan with the most instances per CU (LDS image within
@@ -201,7 +204,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
 // step kind).  Results are memoised per structure within the process.
 bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                       const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu = 163840,
-                      int max_per_cu = 4);
+                      int max_per_cu = 4, int waves = 1);
 
 // ---- lds_layout.cpp: LDS bank-conflict model and optimiser of the solve steps
 // Modelled LDS cycles of one ADMM iteration's solve work for one wave (MI355X_MICROARCH.md, LDS):

@@ -187,11 +187,19 @@ class BatchQP:
     def set_order(self, order):
         """int32 device tensor [B] (kept alive by the handle) or None: a permutation of the
         instance ids, the order in which the persistent launch takes instances (results unchanged;
-        mpcqp_set_order).  The tensor is read at every solve, so it may be rewritten in place."""
+        mpcqp_set_order).  The tensor is read at every solve, so it may be rewritten in place --
+        on the handle's stream, and only with another permutation (a duplicate id would let two
+        waves solve one instance at once; a missing id would never be solved).  It is checked to
+        be a permutation here, once."""
         if order is not None:
             if order.dtype != torch.int32 or tuple(order.shape) != (self.B,) or \
                     not order.is_cuda or not order.is_contiguous():
                 raise ValueError(f"order must be a contiguous int32 tensor of shape ({self.B},)")
+            with torch.cuda.stream(self.stream):
+                ok = torch.equal(torch.sort(order).values,
+                                 torch.arange(self.B, dtype=torch.int32, device=order.device))
+            if not ok:
+                raise ValueError("order must be a permutation of the instance ids 0..B-1")
         check(_lib.lib().mpcqp_set_order(self._h, None if order is None else order.data_ptr()),
               "mpcqp_set_order")
         self._order = order

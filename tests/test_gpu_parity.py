@@ -187,3 +187,7 @@ def test_solve_order_does_not_change_results(golden):
         assert np.array_equal(outs[0][k][solved], outs[2][k][solved], equal_nan=True)
     with pytest.raises(ValueError):
         BatchQP(prob.P, prob.A, batch=4, **st).set_order(torch.zeros(3, dtype=torch.int32))
+    # not a permutation (a duplicate id, a missing id): refused
+    with pytest.raises(ValueError):
+        BatchQP(prob.P, prob.A, batch=4, **st).set_order(
+            torch.tensor([0, 1, 1, 3], dtype=torch.int32, device="cuda"))

@@ -20,9 +20,14 @@ def _kkt(P, A, sigma, rho):
     return sp.bmat([[Pf + sigma * sp.eye(n), A.T], [A, -sp.diags(1.0 / rho)]], format="csc")
 
 
+@pytest.mark.parametrize("waves", ["1", "2"])
 @pytest.mark.parametrize("Nx,dv", [(20, False), (40, True)])
-def test_emulated_schedule_solves_kkt(Nx, dv):
+def test_emulated_schedule_solves_kkt(monkeypatch, Nx, dv, waves):
+    """waves 2: the plan laid out for two waves per instance (every target of a step in one half
+    of the segment positions, symbolic.cpp) solves the same system"""
     from conftest import problem
+
+    monkeypatch.setenv("MPCQP_WAVES", waves)
 
     prob = problem(Nx, dv)
     P, A = triu_csc(prob.P), sorted_csc(prob.A)
@@ -61,16 +66,18 @@ def test_layout_optimiser_lowers_modelled_lds_cycles(monkeypatch):
     assert tot(opt) < 0.8 * tot(greedy), (opt, greedy)
 
 
+@pytest.mark.parametrize("waves", ["1", "2"])
 @pytest.mark.parametrize("copy_rows", ["4", "2", "0"])
 @pytest.mark.parametrize("paired", ["0", "1"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_emulated_schedule_random_structures(monkeypatch, paired, seed, copy_rows):
+def test_emulated_schedule_random_structures(monkeypatch, paired, seed, copy_rows, waves):
     """both step kinds (paired: segments 0 + 1 of a lane on one target, 3 atomics; unpaired: 4)
     solve the KKT system of random sparse QPs, not only the MPC structure the planner was tuned on;
     with the product's copy rows and last-level fold (4), the identity term folded everywhere (2)
     and block-0 copy rows only (0)"""
     monkeypatch.setenv("MPCQP_PAIRED", paired)
     monkeypatch.setenv("MPCQP_COPY_ROWS", copy_rows)
+    monkeypatch.setenv("MPCQP_WAVES", waves)
     rng = np.random.default_rng(100 + seed)
     n, m = 70 + 13 * seed, 110 + 17 * seed
     # within the residual layout's widths (rows of A <= 8 terms, symmetric rows of P <= 4)

@@ -8,7 +8,7 @@ N=${2:-1}; shift 2
 for r in $(seq 1 $N); do
   for L in "$@"; do
     tag=$(basename $L .so)
-    MPCQP_LIBRARY=$R/$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-config3 $AB_ARGS > "$O/${tag}_$r.json" 2> "$O/${tag}_$r.err" || { echo "$tag failed"; tail -5 "$O/${tag}_$r.err"; exit 1; }
+    MPCQP_LIBRARY=$R/$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-legs $AB_ARGS > "$O/${tag}_$r.json" 2> "$O/${tag}_$r.err" || { echo "$tag failed"; tail -5 "$O/${tag}_$r.err"; exit 1; }
     python -c "import json;d=json.load(open('$O/${tag}_$r.json'));print('$tag', round(d['value']), 'waves/cu', d['schedule']['waves_per_cu'], 'lds', d['schedule']['lds_bytes'], 'kernel ms', round(d['roofline']['kernel_ms_per_launch'],2), 'iters', round(d['admm_iters']['mean'],2), 'cold', round(d['cold']['value']), 'cold kernel ms', round(d['cold']['kernel_ms_per_launch'],2))"
   done
 done

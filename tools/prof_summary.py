@@ -36,6 +36,12 @@ def main():
         "bench_hip_event_ms_per_launch": bench["roofline"]["kernel_ms_per_launch"],
         "agreement": float(timed.mean() / bench["roofline"]["kernel_ms_per_launch"]),
         "vgpr": int(r0["VGPR_Count"]), "agpr": int(r0["Accum_VGPR_Count"]),
+        # rocprofv3 derives VGPR_Count from the code object's granulated register count with the
+        # pre-gfx90a granule of 4; gfx950's unified VGPR + AGPR file is allocated in granules of 8
+        # (MI355X_MICROARCH.md, Register files), so the registers a wave holds are twice the
+        # reported count, AGPRs included (Accum_VGPR_Count reads 0): 208 -> 416 >= 256 + 154
+        "unified_regs_allocated": 2 * int(r0["VGPR_Count"]),
+        "waves_per_simd_by_regs": min(8, 512 // (2 * int(r0["VGPR_Count"]))),
         "sgpr": int(r0["SGPR_Count"]), "lds_bytes": int(r0["LDS_Block_Size"]),
         "scratch": int(r0["Scratch_Size"]), "workgroup": int(r0["Workgroup_Size_X"]),
         "grid": int(r0["Grid_Size_X"]),

@@ -6,7 +6,7 @@
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-prof}"; mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --no-cpu-baseline --no-config3"
+B="python3 $R/bench.py --no-cpu-baseline --no-legs"
 timeout -k 10 400 python3 $R/bench.py > "$O/bench.json" 2> "$O/bench.err" || { echo bench failed; tail -5 "$O/bench.err"; exit 1; }
 echo "bench: $(head -c 300 $O/bench.json)"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- $B > "$O/trace_bench.json" 2> "$O/trace.err" || { echo trace failed; tail -5 "$O/trace.err"; exit 1; }
