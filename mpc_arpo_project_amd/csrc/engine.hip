@@ -367,6 +367,62 @@ __device__ __forceinline__ void run_body(Rsrc rs, int n, uint32_t lane, const Op
   }
 }
 #undef MPCQP_STEP
+// Solve steps with the matrix operands read one step ahead (Plan::mat_first: a = the matrix value
+// of every term, constant during a solve): a step issues its 8 vector reads (which follow the
+// previous step's atomics in the LDS queue), then the 8 matrix reads of the next step, then its
+// products -- which wait only for the vector reads (LDS returns in order: a counted lgkmcnt) --
+// and atomics.  The critical path of a step loses 8 of its 16 reads (tools/lds_probe.hip, split
+// step: -13 % per step at two waves per CU, -7 % at four).
+template <bool PAIRED>
+__device__ __forceinline__ void solve_step_pf(const SolveRec& r, const SolveRec& nx, double (&m)[8],
+                                              double* v) {
+  double y[8], mn[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) y[c] = lds_ld(v, r.b[c]);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) mn[c] = lds_ld(v, nx.a[c]);
+  __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+  __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+  const double n0 = fma(-m[1], y[1], -(m[0] * y[0]));
+  const double n1 = fma(-m[3], y[3], -(m[2] * y[2]));
+  const double n2 = fma(-m[5], y[5], -(m[4] * y[4]));
+  const double n3 = fma(-m[7], y[7], -(m[6] * y[6]));
+  if constexpr (PAIRED) {
+    lds_add(r.t0, n0 + n1);
+  } else {
+    lds_add(r.t0, n0);
+    lds_add(r.t1, n1);
+  }
+  lds_add(r.t2, n2);
+  lds_add(r.t3, n3);
+  LDS_FENCE();
+#pragma unroll
+  for (int c = 0; c < 8; ++c) m[c] = mn[c];
+}
+#define MPCQP_PFSTEP(X, Y)                                  \
+  solve_step_pf<PAIRED>(p.X, p.Y, m, v);                    \
+  if (++s >= n) break;                                      \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  load_solve(rs, step_off<SolveOps<PAIRED>>(n, s + 2), lane, p.X); \
+  __builtin_amdgcn_sched_barrier(0);
+template <bool PAIRED>
+struct SolveOps;
+template <bool PAIRED>
+__device__ __forceinline__ void run_body_pf(Rsrc rs, int n, uint32_t lane, double* v,
+                                            Pipe<SolveOps<PAIRED>>& p) {
+  double m[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) m[c] = lds_ld(v, p.a.a[c]);  // the first step's matrix operands
+  int s = 0;
+  for (;;) {
+    MPCQP_PFSTEP(a, b) MPCQP_PFSTEP(b, c) MPCQP_PFSTEP(c, a)
+    MPCQP_PFSTEP(a, b) MPCQP_PFSTEP(b, c) MPCQP_PFSTEP(c, a)
+    MPCQP_PFSTEP(a, b) MPCQP_PFSTEP(b, c) MPCQP_PFSTEP(c, a)
+    MPCQP_PFSTEP(a, b) MPCQP_PFSTEP(b, c) MPCQP_PFSTEP(c, a)
+  }
+}
+#undef MPCQP_PFSTEP
+
 template <bool PAIRED>
 struct SolveOps {
   typedef SolveRec Rec;
@@ -1113,7 +1169,7 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
   LDS_FENCE();
 }
 
-template <int RN, int RM, bool PAIRED>
+template <int RN, int RM, bool PAIRED, bool MATPF>
 __device__ __forceinline__ void solve_instance(const KParams& p, int inst, double* v, double* scr,
                                                int lane) {
   const DevPlan& P = p.pl;
@@ -1254,7 +1310,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     T_END(T_VEC, t_v0);
     T_END(T_V0, t_v0);
     T_BEGIN(t_fw);
-    run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
+    if constexpr (MATPF)
+      run_body_pf<PAIRED>(rs_fwd, P.nfwd, (uint32_t)lane, v, sp);
+    else
+      run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
     T_END(T_FWD, t_fw);
     T_BEGIN(t_v1);
     prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
@@ -1278,7 +1337,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     T_END(T_VEC, t_v1);
     T_END(T_V1, t_v1);
     T_BEGIN(t_bw);
-    run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
+    if constexpr (MATPF)
+      run_body_pf<PAIRED>(rs_bwd, P.nbwd, (uint32_t)lane, v, sp);
+    else
+      run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
     T_END(T_BWD, t_bw);
     T_BEGIN(t_v2);
     // x, z, y updates (auxil.c update_x / update_z / update_y).  The solution reads are issued
@@ -1444,7 +1506,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #ifndef MPCQP_WAVES_PER_EU
 #define MPCQP_WAVES_PER_EU 1
 #endif
-template <int RN, int RM, bool PAIRED>
+template <int RN, int RM, bool PAIRED, bool MATPF>
 __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = (int)threadIdx.x;
@@ -1454,11 +1516,14 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
 #ifdef MPCQP_PAD_AGPR
   // diagnostic builds only (the > 190-AGPR shard-overlap cliff): MPCQP_PAD_AGPR extra
   // accumulation registers held live across the whole kernel, nothing else changed
+#ifndef MPCQP_PAD_KIND
+#define MPCQP_PAD_KIND "+a"  // "+v": the pad in arch VGPRs instead
+#endif
   uint32_t pad[MPCQP_PAD_AGPR];
 #pragma unroll
   for (int k = 0; k < MPCQP_PAD_AGPR; ++k) {
     pad[k] = (uint32_t)k * 2654435761u + (uint32_t)threadIdx.x;
-    asm volatile("" : "+a"(pad[k]));
+    asm volatile("" : MPCQP_PAD_KIND(pad[k]));
   }
 #endif
   for (;;) {
@@ -1476,14 +1541,14 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
     // is not hoisted out of the instance loop (held in registers for the whole kernel it spills)
     int ilane = lane;
     if constexpr (RN >= 4) asm volatile("" : "+v"(ilane));
-    solve_instance<RN, RM, PAIRED>(p, (int)inst, v, scr, ilane);
+    solve_instance<RN, RM, PAIRED, MATPF>(p, (int)inst, v, scr, ilane);
     LDS_FENCE();
   }
 #ifdef MPCQP_PAD_AGPR
   uint32_t acc = 0;
 #pragma unroll
   for (int k = 0; k < MPCQP_PAD_AGPR; ++k) {
-    asm volatile("" : "+a"(pad[k]));
+    asm volatile("" : MPCQP_PAD_KIND(pad[k]));
     acc ^= pad[k];
   }
   if (acc == 0x12345678u && p.timing) p.timing[0] = acc;  // keeps the pad live; never true in practice
@@ -1515,26 +1580,39 @@ int cap_m() { return env_int("MPCQP_CAPM", 0); }  // 0: chosen per structure
 int cap_w() { return env_int("MPCQP_CAPW", 0); }
 
 template <int RN, int RM>
-kernel_fn pick(bool paired, int waves) {
-  if (waves == 2)
-    return paired ? qp_pair_kernel<RN / 2, RM / 2, true> : qp_pair_kernel<RN / 2, RM / 2, false>;
-  return paired ? qp_batch_kernel<RN, RM, true> : qp_batch_kernel<RN, RM, false>;
+kernel_fn pick(bool paired, int waves, bool matpf) {
+  if (waves == 3)  // two waves, the solve steps on the first
+    return paired ? qp_pair_kernel<RN / 2, RM / 2, true, 2> : qp_pair_kernel<RN / 2, RM / 2, false, 2>;
+  if (waves == 2) {
+    if (matpf)
+      return paired ? qp_pair_kernel<RN / 2, RM / 2, true, 1> : qp_pair_kernel<RN / 2, RM / 2, false, 1>;
+    return paired ? qp_pair_kernel<RN / 2, RM / 2, true, 0> : qp_pair_kernel<RN / 2, RM / 2, false, 0>;
+  }
+  if (matpf)
+    return paired ? qp_batch_kernel<RN, RM, true, true> : qp_batch_kernel<RN, RM, false, true>;
+  return paired ? qp_batch_kernel<RN, RM, true, false> : qp_batch_kernel<RN, RM, false, false>;
 }
 
 // RN = ceil(n/64) and RM = ceil(m/64) rounded up to the instantiated buckets; the plan's step kind
 // and waves per instance
-kernel_fn select_kernel(int n, int m, bool paired, int waves) {
+kernel_fn select_kernel(int n, int m, bool paired, int waves, bool matpf) {
   int rn = 0, rm = 0;
   if (!kernel_bucket(n, m, rn, rm)) return nullptr;
-  if (rn == 2) return pick<2, 4>(paired, waves);
+  if (rn == 2) return pick<2, 4>(paired, waves, matpf);
 #ifndef MPCQP_ONLY_SMALL
-  if (rn == 4) return pick<4, 8>(paired, waves);
+  if (rn == 4) return pick<4, 8>(paired, waves, matpf);
 #endif
   return nullptr;
 }
 
-// waves per instance of the solve kernel (MPCQP_WAVES: 1 or 2; DESIGN.md, Two waves per instance)
-int waves_per_instance() { return env_int("MPCQP_WAVES", 1) == 2 ? 2 : 1; }
+// waves per instance of the solve kernel (MPCQP_WAVES: 1; 2 = two waves, solve steps split
+// between them; 3 = two waves, solve steps on the first; DESIGN.md, Two waves per instance)
+int waves_per_instance() {
+  const int w = env_int("MPCQP_WAVES", 1);
+  return (w == 2 || w == 3) ? w : 1;
+}
+// matrix operands of the solve steps read one step ahead (MPCQP_MATPF: 0 or 1; Plan::mat_first)
+bool matrix_prefetch() { return env_int("MPCQP_MATPF", 0) == 1; }
 
 template <typename T>
 size_t push_blob(std::vector<char>& blob, const std::vector<T>& v) {
@@ -1629,7 +1707,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   h->stream = (hipStream_t)stream;
   const int waves = waves_per_instance();
   if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, h->plan, cap_m(), cap_w(),
-                        163840, 4, waves)) {
+                        163840, 4, waves, matrix_prefetch())) {
     std::string e = h->plan.error;
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, e);
@@ -1649,7 +1727,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     return fail(code, msg);
   };
   {
-    h->kern = select_kernel(pl.n, pl.m, pl.paired, pl.waves);
+    h->kern = select_kernel(pl.n, pl.m, pl.paired,
+                            pl.waves == 2 ? (pl.split_steps ? 2 : 3) : 1, pl.mat_first);
     if (!h->kern) {
       delete h;
       return fail(MPCQP_E_UNSUPPORTED, "problem dimensions exceed the instantiated kernels");
@@ -1971,7 +2050,7 @@ int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t
   if (!st || !nnzL) return fail(MPCQP_E_INVALID, "null argument");
   Plan pl;
   if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w(), 163840,
-                        4, waves_per_instance()))
+                        4, waves_per_instance(), matrix_prefetch()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   const int cap = *nnzL;
   *nnzL = pl.nnzL;
@@ -1995,7 +2074,7 @@ int mpcqp_schedule_check(const mpcqp_structure* st, const double* Px, const doub
   if (!st || !Px || !Ax || !rho_vec || !rhs || !sol) return fail(MPCQP_E_INVALID, "null argument");
   Plan pl;  // the plan mpcqp_create would build (MPCQP_WAVES included)
   if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w(), 163840,
-                        4, waves_per_instance()))
+                        4, waves_per_instance(), matrix_prefetch()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   if (model) {
     const LdsModel md = model_lds(pl);

@@ -225,6 +225,7 @@ struct Opt {
     };
     Step best = s;
     int bestc = cur;
+    const bool no_flip = pl.mat_first || getenv("MPCQP_NO_FLIP") != nullptr;
     for (int it = 0; it < moves; ++it) {
       if (cur < bestc) bestc = cur, best = s;
       const double T = T0 * std::pow(T1 / T0, (double)it / moves);
@@ -254,7 +255,7 @@ struct Opt {
         int p2 = rng.below(256);
         if (p2 == p1) continue;
         // two waves per instance: a segment stays in its wave's half (positions 0 + 1 / 2 + 3)
-        if (pl.waves == 2 && (p1 / 128) != (p2 / 128)) continue;
+        if (pl.split_steps && (p1 / 128) != (p2 / 128)) continue;
         std::swap(s[p1], s[p2]);
         const bool ok = lane_ok(p1 % 64) && lane_ok(p2 % 64);
         std::swap(s[p1], s[p2]);
@@ -275,6 +276,10 @@ struct Opt {
           std::swap(s[p1], s[p2]);
         }
       } else if (kind < 6) {  // flip the operands of one term
+        // Plan::mat_first (or MPCQP_NO_FLIP, diagnostics): keep every term's matrix operand first
+        // (a = matrix, b = vector), the convention the matrix-operand prefetch of the solve steps
+        // relies on
+        if (no_flip) continue;
         const int p = used[rng.below((int)used.size())], j = rng.below(2);
         if (s[p].a[j] < 0) continue;
         const int q = p / 64, l = p % 64;

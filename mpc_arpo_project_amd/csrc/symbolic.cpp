@@ -179,7 +179,7 @@ int pack_solve_level_free(const std::vector<Task>& tasks, const Plan& pl, std::v
   // rest.  half[] per segment: 0 / 1 (only the positions of that half are offered to it)
   std::vector<int> half(segs.size(), -1);
   std::vector<size_t> cut;  // step boundaries over segs (two-wave split only)
-  if (pl.waves == 2) {
+  if (pl.split_steps) {
     // tasks by segment count, largest first (a better two-way partition of each step)
     {
       std::vector<std::pair<size_t, size_t>> runs;  // (begin, end) of each task's segments
@@ -222,7 +222,7 @@ int pack_solve_level_free(const std::vector<Task>& tasks, const Plan& pl, std::v
     half.swap(oh);
   }
   for (size_t s0 = 0, ci = 0; s0 < segs.size(); ++ci) {
-    const size_t s1 = pl.waves == 2 ? s0 + cut[ci] : std::min(segs.size(), s0 + 256);
+    const size_t s1 = pl.split_steps ? s0 + cut[ci] : std::min(segs.size(), s0 + 256);
     const size_t base = tbl.size();
     tbl.resize(base + SOLVE_STEP_WORDS, zb);
     uint32_t* terms = tbl.data() + base;
@@ -319,7 +319,7 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
     // an odd count), otherwise to the singles; what does not fit waits for the next step.
     // unit_half[u]: 0 pair lane (one or two segments), 1 single position
     std::vector<int> unit_half;
-    if (pl.waves == 2) {
+    if (pl.split_steps) {
       std::vector<int> ord(rem.size());
       for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
       std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return rem[x].size() > rem[y].size(); });
@@ -376,7 +376,7 @@ int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector
             pairs--;
         }
     }
-    if (pl.waves != 2) unit_half.assign(units.size(), -1);
+    if (!pl.split_steps) unit_half.assign(units.size(), -1);
     // placement: the free position whose operands and target collide least with those placed
     // (ds_read_b64: two 32-lane halves, bank = slot mod 32, broadcast; ds_add_f64: four 16-lane
     // groups, bank = slot mod 16) -- the layout optimiser refines it
@@ -766,7 +766,10 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
                 const int32_t* Ai, Plan& pl, int capM, int capW, bool paired, int waves) {
   pl = Plan();
   pl.paired = paired;
-  pl.waves = waves == 2 ? 2 : 1;
+  // waves: 1; 2 = two waves per instance, solve steps split between them; 3 = two waves per
+  // instance, solve steps on the first (Plan::waves / split_steps)
+  pl.waves = waves >= 2 ? 2 : 1;
+  pl.split_steps = waves == 2;
   pl.n = n, pl.m = m, pl.nk = n + m;
   const int nk = n + m;
   pl.nnzP = Pp[n];
@@ -1430,12 +1433,13 @@ void finish_copy_masks(Plan& pl) {
 
 bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                       const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu,
-                      int max_per_cu, int waves) {
+                      int max_per_cu, int waves, bool mat_first) {
   // the LDS layout optimiser runs on the chosen plan (MPCQP_NO_ANNEAL=1: off, diagnostics)
   const bool anneal = !getenv("MPCQP_NO_ANNEAL") && !getenv("MPCQP_NO_LAYOUT");
   const char* fp = getenv("MPCQP_PAIRED");  // diagnostics: force the step kind
   if (capM > 0 && capW > 0) {
     if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW, !fp || atoi(fp) != 0, waves)) return false;
+    plan.mat_first = mat_first;
     if (anneal) optimize_lds(plan);
     finish_copy_masks(plan);
     return true;
@@ -1445,6 +1449,7 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
   std::vector<int32_t> key;
   key.push_back(n), key.push_back(m), key.push_back(lds_per_cu), key.push_back(max_per_cu);
   key.push_back(waves);
+  key.push_back(mat_first);
   key.push_back(anneal);
   key.push_back(fp ? atoi(fp) : -1);
   const char* cm = getenv("MPCQP_COPY_ROWS");  // diagnostics: the copy-row mode (build_plan)
@@ -1494,6 +1499,7 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
   if (!found) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);  // reports the error
   if (getenv("MPCQP_DUMP_CAPS")) fprintf(stderr, "caps %d %d paired %d\n", bm, bw, (int)bp);
   if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw, bp, waves)) return false;
+  plan.mat_first = mat_first;
   if (anneal) optimize_lds(plan);
   finish_copy_masks(plan);
   {

@@ -163,6 +163,14 @@ struct Plan {
   // segment positions 0 + 1 of every lane, wave 1 positions 2 + 3; within a step every target's
   // segments sit in one of the two halves, so each target is summed by one wave in a fixed order
   int waves = 1;
+  // two waves per instance: the solve steps split between them (true: wave 0 executes segment
+  // positions 0 + 1, wave 1 positions 2 + 3, the packing constraint above) or all executed by the
+  // first wave while the second waits (false)
+  bool split_steps = false;
+  // every solve term keeps its matrix operand first (segment words a = matrix value, b = vector
+  // entry; the layout optimiser does not flip operands): the kernel then reads the matrix operands
+  // of the next step during the current one (they are constant during a solve)
+  bool mat_first = false;
   // two-wave kernel: LDS slots (doubles) of the cross-wave exchange (XCH_DOUBLES: two buffers x two
   // waves x XCH_K values) and of the instance id the first wave hands the second (XID)
   int XCH = 0, XID = 0;
@@ -204,7 +212,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
 // step kind).  Results are memoised per structure within the process.
 bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                       const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu = 163840,
-                      int max_per_cu = 4, int waves = 1);
+                      int max_per_cu = 4, int waves = 1, bool mat_first = false);
 
 // ---- lds_layout.cpp: LDS bank-conflict model and optimiser of the solve steps
 // Modelled LDS cycles of one ADMM iteration's solve work for one wave (MI355X_MICROARCH.md, LDS):
