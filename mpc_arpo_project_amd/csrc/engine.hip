@@ -1606,10 +1606,24 @@ kernel_fn select_kernel(int n, int m, bool paired, int waves, bool matpf) {
 }
 
 // waves per instance of the solve kernel (MPCQP_WAVES: 1; 2 = two waves, solve steps split
-// between them; 3 = two waves, solve steps on the first; DESIGN.md, Two waves per instance)
+// between them; 3 = two waves, solve steps on the first; unset or 0: chosen per structure by
+// auto_waves; DESIGN.md, Two waves per instance)
 int waves_per_instance() {
-  const int w = env_int("MPCQP_WAVES", 1);
-  return (w == 2 || w == 3) ? w : 1;
+  const int w = env_int("MPCQP_WAVES", 0);
+  return (w == 1 || w == 2 || w == 3) ? w : 0;
+}
+// The automatic choice: two waves per instance with the solve steps on the first (3) when the
+// one-wave image leaves at most two instances per CU -- then two of the CU's four SIMDs would idle,
+// and the second wave takes half of the vector passes, checks and Ruiz passes onto them (N = 40:
+// +8 % solves/s, profiles/r04/pair2); one wave otherwise (N = 20: four instances per CU, where the
+// second wave's barriers cost more than its share saves: -4 %)
+int auto_waves(const mpcqp_structure* st) {
+  Plan p1;
+  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, p1, cap_m(), cap_w(), 163840,
+                        4, 1, false))
+    return 1;
+  const int bytes = ((p1.LDS_N + 1) & ~1) * 8;
+  return 163840 / std::max(bytes, 1) <= 2 ? 3 : 1;
 }
 // matrix operands of the solve steps read one step ahead (MPCQP_MATPF: 0 or 1; Plan::mat_first)
 bool matrix_prefetch() { return env_int("MPCQP_MATPF", 0) == 1; }
@@ -1705,7 +1719,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   h->set = *s;
   h->B = batch;
   h->stream = (hipStream_t)stream;
-  const int waves = waves_per_instance();
+  int waves = waves_per_instance();
+  if (waves == 0) waves = auto_waves(st);
   if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, h->plan, cap_m(), cap_w(),
                         163840, 4, waves, matrix_prefetch())) {
     std::string e = h->plan.error;
@@ -2050,7 +2065,8 @@ int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t
   if (!st || !nnzL) return fail(MPCQP_E_INVALID, "null argument");
   Plan pl;
   if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w(), 163840,
-                        4, waves_per_instance(), matrix_prefetch()))
+                        4, waves_per_instance() ? waves_per_instance() : auto_waves(st),
+                        matrix_prefetch()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   const int cap = *nnzL;
   *nnzL = pl.nnzL;
@@ -2074,7 +2090,8 @@ int mpcqp_schedule_check(const mpcqp_structure* st, const double* Px, const doub
   if (!st || !Px || !Ax || !rho_vec || !rhs || !sol) return fail(MPCQP_E_INVALID, "null argument");
   Plan pl;  // the plan mpcqp_create would build (MPCQP_WAVES included)
   if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w(), 163840,
-                        4, waves_per_instance(), matrix_prefetch()))
+                        4, waves_per_instance() ? waves_per_instance() : auto_waves(st),
+                        matrix_prefetch()))
     return fail(MPCQP_E_UNSUPPORTED, pl.error);
   if (model) {
     const LdsModel md = model_lds(pl);

@@ -20,7 +20,7 @@ def _kkt(P, A, sigma, rho):
     return sp.bmat([[Pf + sigma * sp.eye(n), A.T], [A, -sp.diags(1.0 / rho)]], format="csc")
 
 
-@pytest.mark.parametrize("waves", ["1", "2"])
+@pytest.mark.parametrize("waves", ["1", "2", "3"])
 @pytest.mark.parametrize("Nx,dv", [(20, False), (40, True)])
 def test_emulated_schedule_solves_kkt(monkeypatch, Nx, dv, waves):
     """waves 2: the plan laid out for two waves per instance (every target of a step in one half
@@ -66,7 +66,7 @@ def test_layout_optimiser_lowers_modelled_lds_cycles(monkeypatch):
     assert tot(opt) < 0.8 * tot(greedy), (opt, greedy)
 
 
-@pytest.mark.parametrize("waves", ["1", "2"])
+@pytest.mark.parametrize("waves", ["1", "2", "3"])
 @pytest.mark.parametrize("copy_rows", ["4", "2", "0"])
 @pytest.mark.parametrize("paired", ["0", "1"])
 @pytest.mark.parametrize("seed", [1, 2])
