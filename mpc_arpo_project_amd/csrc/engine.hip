@@ -1581,8 +1581,12 @@ int cap_w() { return env_int("MPCQP_CAPW", 0); }
 
 template <int RN, int RM>
 kernel_fn pick(bool paired, int waves, bool matpf) {
-  if (waves == 3)  // two waves, the solve steps on the first
-    return paired ? qp_pair_kernel<RN / 2, RM / 2, true, 2> : qp_pair_kernel<RN / 2, RM / 2, false, 2>;
+  // two waves, the solve steps on the first; MPCQP_W0DIAG=1: the diagonal pass too (mode 3,
+  // measured equal to mode 2 at N = 40)
+  if (waves == 3)
+    return env_int("MPCQP_W0DIAG", 0)
+               ? (paired ? qp_pair_kernel<RN / 2, RM / 2, true, 3> : qp_pair_kernel<RN / 2, RM / 2, false, 3>)
+               : (paired ? qp_pair_kernel<RN / 2, RM / 2, true, 2> : qp_pair_kernel<RN / 2, RM / 2, false, 2>);
   if (waves == 2) {
     if (matpf)
       return paired ? qp_pair_kernel<RN / 2, RM / 2, true, 1> : qp_pair_kernel<RN / 2, RM / 2, false, 1>;

@@ -15,6 +15,6 @@ if [ -z "$GC_SKIP_TESTS" ]; then
   tail -1 "$O/smoke.log"
 fi
 timeout -k 10 600 python bench.py > "$O/bench.json" 2> "$O/bench.err" || { echo bench failed; tail -20 "$O/bench.err"; exit 1; }
-python -c "import json;d=json.load(open('$O/bench.json'));print('bench', round(d['value']), d['admm_iters'], 'frac', round(d['roofline']['frac'],4), 'config3', round(d['config3'].get('value',0)), 'cpu', round(d.get('cpu_baseline',{}).get('value',0)))"
+python -c "import json;d=json.load(open('$O/bench.json'));print('bench', round(d['value']), d['admm_iters'], 'frac', round(d['roofline']['frac'],4), 'config3', round(d['config3'].get('value',0)), 'n40_accel', round(d['n40_accel'].get('value',0)), 'config4', round(d['config4'].get('value',0)), 'cpu', round(d.get('cpu_baseline',{}).get('value',0)))"
 timeout -k 10 600 python bench.py --continuous --steps ${GC_CONT_STEPS:-5} --warmup 1 > "$O/bench_cont.json" 2> "$O/bench_cont.err" || { echo cont bench failed; tail -20 "$O/bench_cont.err"; exit 1; }
 python -c "import json;d=json.load(open('$O/bench_cont.json'));print('continuous', round(d['value']), d['period_split_ms'], d['admm_iters'])"
