@@ -176,14 +176,14 @@ def closed_loop_run(prob, X0, B, K, W, S, eps, rank, device, dist=None, track=No
     engine solved it (active: not terminated).  track: (nsim, dist_tol, ang_tol) -> per-chaser
     run summaries (enable_tracking)."""
     import torch
-    from mpc_arpo_project_amd.closed_loop import BatchClosedLoop
+    from mpc_arpo_project_amd.closed_loop import BatchClosedLoop, shard_streams
 
     cut = [B * j // S for j in range(S + 1)]
     cls = []
+    sts = shard_streams(device, S) if S > 1 else [None]  # the same streams for every leg
     for j in range(S):
-        st_j = torch.cuda.Stream(device=device) if S > 1 else None
         cls.append(BatchClosedLoop(prob, X0[cut[j]:cut[j + 1]], device=device, eps_abs=eps,
-                                   eps_rel=eps, stream=st_j, id_offset=rank * B + cut[j],
+                                   eps_rel=eps, stream=sts[j], id_offset=rank * B + cut[j],
                                    longest_first=longest_first))
         if track:
             cls[-1].enable_tracking(*track)
@@ -269,7 +269,7 @@ def roofline(run, S, K, elapsed):
     lds_ach = float(lds_b.sum() / elapsed) / 1e9
     return dict(
         bound="lds", achieved=lds_ach, peak=LDS_PEAK_GBS, unit="GB/s", frac=lds_ach / LDS_PEAK_GBS,
-        traffic=None, kernel="qp_batch_kernel", kernel_ms_per_launch=float(np.mean(kt) * 1e3),
+        traffic=None, kernel=kernel_name(sched), kernel_ms_per_launch=float(np.mean(kt) * 1e3),
         concurrent_shards=S, lds_bytes_per_iter=lds_iter,
         admm_iters_timed=float(itm.sum()),
         lds_bytes_per_launch=float(lds_b.mean()),
@@ -409,12 +409,17 @@ def bench_discrete(args, rank, world, device, dist):
     return out
 
 
-def lds_roof(iters_total, lds_iter, seconds, kernel_ms=None, fp64=None):
+def kernel_name(sched):
+    """the solve kernel a handle launches: one wave per instance, or two"""
+    return "qp_pair_kernel" if sched.get("waves_per_instance", 1) == 2 else "qp_batch_kernel"
+
+
+def lds_roof(iters_total, lds_iter, seconds, kernel_ms=None, fp64=None, kernel="qp_batch_kernel"):
     """LDS-graded roofline of a leg: the LDS bytes its solve launches moved (ADMM iterations x
     lds_bytes_per_iter) over the leg's timed wall time."""
     ach = iters_total * lds_iter / seconds / 1e9
     out = {"bound": "lds", "achieved": ach, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-           "frac": ach / LDS_PEAK_GBS, "traffic": None, "kernel": "qp_batch_kernel",
+           "frac": ach / LDS_PEAK_GBS, "traffic": None, "kernel": kernel,
            "lds_bytes_per_iter": lds_iter, "admm_iters_timed": float(iters_total)}
     if kernel_ms is not None:
         out["kernel_ms_per_launch"] = kernel_ms
@@ -528,7 +533,8 @@ def bench_continuous(args, rank, world, device, dist):
     it_timed = float(np.where(a, it, 0).sum())
     # graded over the whole timed periods (plant + UKF + configure included); the solve launches
     # alone beside it (their HIP-event time)
-    roof = lds_roof(it_timed, lds_iter, elapsed, kernel_ms=float(t_solve.mean()))
+    roof = lds_roof(it_timed, lds_iter, elapsed, kernel_ms=float(t_solve.mean()),
+                    kernel=kernel_name(sched))
     roof["frac_over_solve_launches"] = it_timed * lds_iter / (t_solve.sum() * 1e-3) / 1e9 / LDS_PEAK_GBS
     return {
         "metric": f"MPC-QP solves/sec @ N={nx} offset-free MPC in the continuous-time nonlinear "

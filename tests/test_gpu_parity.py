@@ -156,6 +156,35 @@ def test_repeated_solves_are_bit_identical(golden):
             assert np.array_equal(runs[0][k], runs[1][k], equal_nan=True)
 
 
+@pytest.mark.parametrize("Nx,dv,tag", [(20, False, "batch_n20"), (40, True, "batch_n40dv")])
+def test_waves_per_instance_do_not_change_results(golden, monkeypatch, Nx, dv, tag):
+    """the one-wave kernel and the two-wave kernels with the solves on the first wave (modes 2 and
+    3, DESIGN.md Two waves per instance) run the same plan with the same arithmetic order: cold and
+    warm solves are bit-identical (statuses, iterations, x, y)"""
+    from conftest import problem
+
+    prob = problem(Nx, dv)
+    d = golden(tag)
+    B = d["Ax"].shape[0]
+    st = dict(eps_abs=1e-4, eps_rel=1e-4)
+    outs = []
+    for waves, w0diag in (("1", "0"), ("3", "0"), ("3", "1")):
+        monkeypatch.setenv("MPCQP_WAVES", waves)
+        monkeypatch.setenv("MPCQP_W0DIAG", w0diag)
+        qp = BatchQP(prob.P, prob.A, batch=B, **st)
+        qp.set_data(q=prob.q, Ax=d["Ax"][:B], l=d["l"][:B], u=d["u"][:B])
+        got = []
+        for _ in range(2):  # cold, then warm from the first solve's state
+            r = qp.solve()
+            got += [r.status.cpu().numpy(), r.iter.cpu().numpy(), r.x.cpu().numpy(),
+                    r.y.cpu().numpy()]
+        outs.append(got)
+        qp.close()
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b, equal_nan=True)
+
+
 def test_solve_order_does_not_change_results(golden):
     """mpcqp_set_order only changes which wave takes which instance: a random permutation gives
     bit-identical statuses, iterations and solutions, with and without a skip mask"""
