@@ -11,8 +11,9 @@ bit-exactly against the reference's runs; they differ only in who solves the per
     (x, status) back to the device controller.
 
 The runs are chaotic in the solver's rounding (one status flip changes the controller, and every
-later state), so the comparison is made against the oracle's own floor: the oracle-driven run
-repeated from initial states moved by one ulp.  The reference's run reduction is compared:
+later state), so the comparison is made against the oracle's own floor: the oracle-driven run repeated from
+initial states moved by one ulp, and with every solve's right-hand side moved by one ulp
+(floor_run).  The reference's run reduction is compared:
 isSuccess, i_term and the final distance |x(i_term - 1) - xr| (src/trajectorySimulate.py:359-387,
 test/disturbRejComp.py:88)."""
 from __future__ import annotations
@@ -41,7 +42,10 @@ def engine_run(prob, X0, nsim, suc_cond, noise, eps, noise_seed=123, id_offset=0
     return out
 
 
-def oracle_run(prob, X0, nsim, suc_cond, noise, eps, noise_seed=123, id_offset=0, threads=16):
+def oracle_run(prob, X0, nsim, suc_cond, noise, eps, noise_seed=123, id_offset=0, threads=16,
+               jitter=0):
+    """jitter != 0: every solver moves each KKT right-hand side by one ulp before each solve
+    (oracle set_jitter, seeded per chaser) -- the floor of a different summation order"""
     cl = BatchClosedLoop(prob, X0, noise=noise, noise_seed=noise_seed, id_offset=id_offset,
                          eps_abs=eps, eps_rel=eps)
     cl.enable_tracking(nsim, *suc_cond)
@@ -62,6 +66,8 @@ def oracle_run(prob, X0, nsim, suc_cond, noise, eps, noise_seed=123, id_offset=0
                 s = orc.OracleOSQP()
                 s.setup(prob.P, prob.q, A, l[b], u[b], eps_abs=eps, eps_rel=eps,
                         warm_start=True, verbose=False)
+                if jitter:
+                    s.set_jitter(jitter * 1000003 + b + 1)
                 solvers.append(s)
             x, st, it = orc.batch_update_solve([solvers[b] for b in act], None, None, None, threads)
         else:
@@ -108,15 +114,16 @@ def compare(a, b):
 FLOOR_DRAWS = 4
 
 
-def ulp_perturbed(X0, draw=0):
-    """every initial state coordinate moved by one ulp: draw 0 towards +inf, draw 1 towards -inf,
-    later draws up or down at random (seeded by the draw) -- independent floor draws"""
-    if draw == 0:
-        return np.nextafter(X0, np.inf)
-    if draw == 1:
-        return np.nextafter(X0, -np.inf)
-    up = np.random.default_rng(1000 + draw).random(X0.shape) < 0.5
-    return np.where(up, np.nextafter(X0, np.inf), np.nextafter(X0, -np.inf))
+def floor_run(prob, X0, nsim, suc_cond, noise, eps, draw):
+    """one floor draw of the oracle-driven run: draws 0 and 1 start from the initial states moved
+    by one ulp (every nonzero coordinate up, resp. down; exact zeros -- the chasers' initial
+    velocities -- stay zero: a signed denormal there is a branch input, not a rounding), draws 2
+    and 3 keep the initial states and move every KKT right-hand side by one ulp in every solve
+    (two jitter seeds: the backward error of a different summation order, per solve)"""
+    if draw < 2:
+        X = np.where(X0 == 0, X0, np.nextafter(X0, np.inf if draw == 0 else -np.inf))
+        return oracle_run(prob, X, nsim, suc_cond, noise, eps)
+    return oracle_run(prob, X0, nsim, suc_cond, noise, eps, jitter=draw - 1)
 
 
 def floor_bound(floors, key, G):

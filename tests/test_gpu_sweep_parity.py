@@ -3,10 +3,11 @@
 i_term, final distance; src/trajectorySimulate.py:359-387, test/disturbRejComp.py:88) compared
 chaser by chaser.  The closed loops are chaotic in the solver's rounding -- the oracle itself,
 restarted from initial states one ulp away, reproduces only ~70 % of its own runs exactly -- so
-the engine is held to that floor: four independent one-ulp draws of the oracle against itself
-give the floor's spread, and the engine's agreement with the oracle may not fall below the worst
-draw by more than two of the draws' standard deviations (sweep_parity.floor_bound; measured:
-profiles/r04/sweep_parity.json)."""
+the engine is held to that floor: four one-ulp draws of the oracle against itself (two of the
+initial states, two of every solve's right-hand side: sweep_parity.floor_run) give the floor's
+spread, and the engine's agreement with the oracle may not fall below the worst draw by more than
+two of the draws' standard deviations and one scenario (sweep_parity.floor_bound; measured:
+profiles/r04/evidence/parity_printouts.log)."""
 import numpy as np
 import pytest
 
@@ -33,8 +34,8 @@ def test_full_length_sweep_matches_oracle_driven_runs(scenario, nx, noise, rejec
     X0 = sweep.initial_conditions(scenario, 256)
     eng = spp.engine_run(prob, X0, nsim, sim.suc_cond, noise, 1e-3)
     orc = spp.oracle_run(prob, X0, nsim, sim.suc_cond, noise, 1e-3)
-    floors = [spp.compare(spp.oracle_run(prob, spp.ulp_perturbed(X0, d), nsim, sim.suc_cond,
-                                         noise, 1e-3), orc) for d in range(spp.FLOOR_DRAWS)]
+    floors = [spp.compare(spp.floor_run(prob, X0, nsim, sim.suc_cond, noise, 1e-3, d), orc)
+              for d in range(spp.FLOOR_DRAWS)]
     ev = spp.compare(eng, orc)
     G = ev["scenarios"]
     print(scenario, nx, "engine vs oracle", ev)

@@ -37,7 +37,7 @@ def run_case(name, n, eps=1e-3):
     t1 = time.time()
     o = spp.oracle_run(prob, X0, nsim, sim.suc_cond, c["noise"], eps)
     t2 = time.time()
-    o1 = spp.oracle_run(prob, spp.ulp_perturbed(X0), nsim, sim.suc_cond, c["noise"], eps)
+    o1 = spp.floor_run(prob, X0, nsim, sim.suc_cond, c["noise"], eps, 0)
     return dict(case=name, config=dict(c, eps=eps, nsim=nsim), n=n,
                 engine_vs_oracle=spp.compare(e, o), oracle_vs_oracle_ulp=spp.compare(o1, o),
                 seconds=dict(engine=t1 - t0, oracle=t2 - t1))
