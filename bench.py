@@ -155,16 +155,19 @@ def cpu_baseline(prob, X0, steps, warmup, eps, sample, threads, device):
                      "status flip changes its later starting points; see DESIGN.md, Parity")
 
 
-def load_profile(name, B, nx, split):
-    """A committed PMC-derived figure (profiles/current/<name>.json, written by tools/pmc_traffic.py
-    or tools/sq_summary.py on the GPU box) for this workload, with the commit it was measured at."""
-    path = os.path.join(REPO, "profiles", "current", name)
-    try:
-        pj = json.load(open(path))
-        if pj.get("batch") == B and pj.get("nx") == nx and pj.get("concurrent_shards") == split:
+def load_profile(name, B, nx, split, dv=False):
+    """A committed PMC-derived figure (profiles/current/<name>.json or <name>_n<nx>[dv].json,
+    written by tools/pmc_traffic.py or tools/sq_summary.py on the GPU box) for this workload, with
+    the commit it was measured at."""
+    stem = name[:-len(".json")]
+    for fn in (name, f"{stem}_n{nx}{'dv' if dv else ''}.json"):
+        try:
+            pj = json.load(open(os.path.join(REPO, "profiles", "current", fn)))
+        except Exception:
+            continue
+        if (pj.get("batch") == B and pj.get("nx") == nx and pj.get("concurrent_shards") == split
+                and bool(pj.get("dv", False)) == bool(dv)):
             return pj
-    except Exception:
-        pass
     return None
 
 
@@ -287,10 +290,10 @@ def roofline(run, S, K, elapsed):
                                  "iteration); they stay in LDS/VGPRs instead"})
 
 
-def attach_profiles(roof, B, nx, S, K, elapsed):
+def attach_profiles(roof, B, nx, S, K, elapsed, dv=False):
     """HBM traffic (PMC FETCH_SIZE + WRITE_SIZE) and LDS busy share (SQ_LDS_IDX_ACTIVE) from the
     committed profile of this workload, when there is one."""
-    pj = load_profile("pmc_traffic.json", B, nx, S)
+    pj = load_profile("pmc_traffic.json", B, nx, S, dv)
     if pj and pj.get("hbm_bytes_per_launch"):
         t = pj["hbm_bytes_per_launch"]
         ach = t * S * K / elapsed / 1e9
@@ -301,7 +304,7 @@ def attach_profiles(roof, B, nx, S, K, elapsed):
                        "measured_at": pj.get("commit"),
                        "what": "PMC FETCH_SIZE + WRITE_SIZE (L2 <-> fabric, calibrated; "
                                "tools/pmc_run.sh)"}
-    sq = load_profile("sq_summary.json", B, nx, S)
+    sq = load_profile("sq_summary.json", B, nx, S, dv)
     if sq and sq.get("lds_array_busy_fraction_if_per_cu") is not None:
         roof["lds_busy"] = {"frac": sq["lds_array_busy_fraction_if_per_cu"],
                             "bank_conflict_share": sq.get("lds_conflict_share"),
@@ -336,7 +339,7 @@ def bench_discrete(args, rank, world, device, dist):
         elapsed = max(float(x[0]) for x in tt)
         solved = sum(float(x[1]) for x in tt)
     roof = roofline(run, S, K, run["elapsed"])
-    attach_profiles(roof, B, args.nx, S, K, run["elapsed"])
+    attach_profiles(roof, B, args.nx, S, K, run["elapsed"], args.dv)
     if rank != 0:
         for c in cls:
             c.close()
@@ -445,7 +448,7 @@ def bench_leg(args, rank, device, nx, dv):
                           longest_first=args.order == "iters")
     it, act = run["it"], run["act"]
     roof = roofline(run, S, K, run["elapsed"])
-    attach_profiles(roof, B, nx, S, K, run["elapsed"])
+    attach_profiles(roof, B, nx, S, K, run["elapsed"], dv)
     for c in run["cls"]:
         c.close()
     model = "impulsive delta-v" if dv else "continuous acceleration"

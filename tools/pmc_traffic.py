@@ -38,10 +38,11 @@ def main():
     ap.add_argument("--calib-write", required=True)
     ap.add_argument("--bench", required=True, help="bench.py JSON line of the PMC runs' workload")
     ap.add_argument("--calib-bytes", type=float, default=float(1 << 30))
-    ap.add_argument("--kernel", default="qp_batch_kernel")
+    ap.add_argument("--kernel", default=None, help="default: the kernel the bench roofline names")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
+    a.kernel = a.kernel or bench["roofline"].get("kernel", "qp_batch_kernel")
     S = bench["roofline"].get("concurrent_shards", 1)  # solve launches per step (one per shard)
     warm = bench["warmup"] * S
 

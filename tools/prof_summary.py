@@ -16,12 +16,13 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("bench")
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--kernel", default="qp_batch_kernel")
+    ap.add_argument("--kernel", default=None, help="default: the kernel the bench's roofline names")
     a = ap.parse_args()
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
     # the untimed warm-up steps launch the solve kernel once per concurrent shard
     warm = bench["warmup"] * bench["roofline"].get("concurrent_shards", 1) if a.warmup is None else a.warmup
-    rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
+    kname = a.kernel or bench["roofline"].get("kernel", "qp_batch_kernel")
+    rows = [r for r in csv.DictReader(open(a.trace)) if kname in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = np.array([int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]) * 1e-6
     timed = dur[warm:]

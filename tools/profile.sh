@@ -21,7 +21,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU
 echo sq ok
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace40" -o run -- $B --nx 40 --dv > "$O/bench40.json" 2> "$O/bench40.err" || { echo n40 failed; tail -5 "$O/bench40.err"; exit 1; }
 echo "n40: $(head -c 300 $O/bench40.json)"
-timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS -d "$O/sq40" -o run --output-format csv -- $B --nx 40 --dv --steps 5 --warmup 2 > "$O/sq40.json" 2> "$O/sq40.err" || { echo sq40 failed; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$O/sq40" -o run --output-format csv -- $B --nx 40 --dv --steps 5 --warmup 2 > "$O/sq40.json" 2> "$O/sq40.err" || { echo sq40 failed; exit 1; }
 echo sq40 ok
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_cont" -o run -- python3 $R/bench.py --continuous --steps 5 --warmup 1 > "$O/bench_cont.json" 2> "$O/bench_cont.err" || { echo continuous trace failed; tail -5 "$O/bench_cont.err"; exit 1; }
 echo "continuous: $(head -c 300 $O/bench_cont.json)"
