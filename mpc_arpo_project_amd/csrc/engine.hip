@@ -1048,7 +1048,11 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
   double cprev = 1.0;  // cost factor of the last pass, not yet applied to P's values
   double dpc[RN];      // P's column norms before that factor (the cost normalisation's)
   LDS_FENCE();
+#ifdef MPCQP_ABL_NOSCALE  // fixed-work ablation builds only
+  for (int it = 0; it < 0; ++it) {
+#else
   for (int it = 0; it < p.s.scaling; ++it) {
+#endif
     // compute_inf_norm_cols_KKT: columns of [P A'; A 0] (P symmetric from its upper triangle).
     // After the first pass P's column norms are the cost normalisation's norms times its factor
     // c (still pending on P's values): max_k |c x_k| = c max_k |x_k| exactly, rounding being
@@ -1192,7 +1196,9 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   S.rho = (hs != 0) ? p.rho_state[inst] : p.rho0;
   set_rho(S);
   T_BEGIN(t_f0);
+#ifndef MPCQP_ABL_NOFAC  // fixed-work ablation builds only
   assemble_and_factor<RN, RM>(p, sb, v, lane, S);
+#endif
   T_END(T_FACTOR, t_f0);
   T_COUNT(T_NFACT);
 
@@ -1296,27 +1302,34 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     for (int r = 0; r < RN; ++r) {
       xp[r] = S.x[r];
       const double b = sigma * xp[r] - S.q[r];
+#ifndef MPCQP_ABL_NORHS  // fixed-work ablation builds only (Where the time goes)
       v[wsx[r] + coff] = b;
       v[wsx[r]] = and_d(b, wmk[r]);
+#endif
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       zp[r] = S.z[r];
       bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
+#ifndef MPCQP_ABL_NORHS
       v[wsz[r] + coff] = bz[r];
       v[wsz[r]] = and_d(bz[r], wmk[RN + r]);
+#endif
     }
     LDS_FENCE();
     T_END(T_VEC, t_v0);
     T_END(T_V0, t_v0);
     T_BEGIN(t_fw);
+#ifndef MPCQP_ABL_NOSOLVE
     if constexpr (MATPF)
       run_body_pf<PAIRED>(rs_fwd, P.nfwd, (uint32_t)lane, v, sp);
     else
       run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
+#endif
     T_END(T_FWD, t_fw);
     T_BEGIN(t_v1);
     prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
+#ifndef MPCQP_ABL_NODIAG
     {
       // C = (1/D) W; W restarts at 0, or at C where the row's identity term is folded into it
       // (Plan::bcopy: the backward task has no MONE term)
@@ -1333,24 +1346,34 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         v[P.W + lane + 64 * r] = and_d(c, bmk[r]);
       }
     }
+#endif
     LDS_FENCE();
     T_END(T_VEC, t_v1);
     T_END(T_V1, t_v1);
     T_BEGIN(t_bw);
+#ifndef MPCQP_ABL_NOSOLVE
     if constexpr (MATPF)
       run_body_pf<PAIRED>(rs_bwd, P.nbwd, (uint32_t)lane, v, sp);
     else
       run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
+#endif
     T_END(T_BWD, t_bw);
     T_BEGIN(t_v2);
     // x, z, y updates (auxil.c update_x / update_z / update_y).  The solution reads are issued
     // together before any use (otherwise the compiler reuses one register pair for all of them
     // and waits for each read in turn)
     double wx[RN], wz[RM];
+#ifdef MPCQP_ABL_NOUPD  // no solution read-back: the update runs on the previous values
+#pragma unroll
+    for (int r = 0; r < RN; ++r) wx[r] = xp[r];
+#pragma unroll
+    for (int r = 0; r < RM; ++r) wz[r] = zp[r];
+#else
 #pragma unroll
     for (int r = 0; r < RN; ++r) wx[r] = v[wsx[r]];  // the junk slot reads back 0
 #pragma unroll
     for (int r = 0; r < RM; ++r) wz[r] = v[wsz[r]];
+#endif
     __builtin_amdgcn_sched_group_barrier(0x100, RN + RM, 0);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
