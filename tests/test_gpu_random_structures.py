@@ -39,10 +39,15 @@ def _random_qp(seed, B):
     return P, q, A, Ax, l, u
 
 
+@pytest.mark.parametrize("waves", ["0", "2", "3"])
 @pytest.mark.parametrize("paired", ["1", "0"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_random_structures_match_oracle(monkeypatch, paired, seed):
+def test_random_structures_match_oracle(monkeypatch, paired, seed, waves):
+    """waves: MPCQP_WAVES -- 0 the automatic choice (one wave for these sizes), 2 two waves with the
+    solve steps split between them (their own step packing), 3 two waves with the steps on the first
+    (Two waves per instance)"""
     monkeypatch.setenv("MPCQP_PAIRED", paired)
+    monkeypatch.setenv("MPCQP_WAVES", waves)
     B = 96
     P, q, A, Ax, l, u = _random_qp(seed, B)
     st = dict(eps_abs=1e-5, eps_rel=1e-5)
@@ -51,7 +56,7 @@ def test_random_structures_match_oracle(monkeypatch, paired, seed):
     r = qp.solve()
     xo, yo, so, io = orc.batch_solve(P, q, A, Ax, l, u, nthreads=8, **st)
     sg, ig, xg = r.status.cpu().numpy(), r.iter.cpu().numpy(), r.x.cpu().numpy()
-    print(f"paired={paired} seed={seed}: statuses {np.unique(so, return_counts=True)}, "
+    print(f"waves={waves} paired={paired} seed={seed}: statuses {np.unique(so, return_counts=True)}, "
           f"status agreement {np.mean(sg == so):.4f}, iteration agreement {np.mean(ig == io):.4f}")
     assert np.mean(so == 1) >= 0.9  # the generator makes feasible, well-posed QPs
     assert np.array_equal(sg, so)
