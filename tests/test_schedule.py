@@ -21,10 +21,12 @@ def _kkt(P, A, sigma, rho):
 
 
 @pytest.mark.parametrize("waves", ["1", "2", "3"])
-@pytest.mark.parametrize("Nx,dv", [(20, False), (40, True)])
+@pytest.mark.parametrize("Nx,dv", [(20, False), (40, True), (30, False), (40, False), (50, True),
+                                   (51, False)])
 def test_emulated_schedule_solves_kkt(monkeypatch, Nx, dv, waves):
     """waves 2: the plan laid out for two waves per instance (every target of a step in one half
-    of the segment positions, symbolic.cpp) solves the same system"""
+    of the segment positions, symbolic.cpp) solves the same system; the other horizons of the
+    reference's scripts (Nx 20-50) up to the largest the (4, 8) bucket accepts"""
     from conftest import problem
 
     monkeypatch.setenv("MPCQP_WAVES", waves)
