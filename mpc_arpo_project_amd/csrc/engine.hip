@@ -1173,6 +1173,15 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
   LDS_FENCE();
 }
 
+// Register buckets from which the per-lane addresses get an opaque lane id per instance (and per
+// check) instead of being hoisted out of the persistent instance loop: all of them (2).  Hoisted,
+// the addresses of the RN = 2 kernel held ~100 registers across the loop (256 + 154 allocated vs
+// 256 + 50 now, same speed) -- and builds with more register pressure computed wrong results from
+// the second instance a wave takes onward, with every first instance bit-exact (DESIGN.md,
+// High-register builds; tools/cliff_localize.py).  Diagnostics may raise it (4: round-3/4 builds).
+#ifndef MPCQP_OPAQUE_LANE_RN
+#define MPCQP_OPAQUE_LANE_RN 2
+#endif
 template <int RN, int RM, bool PAIRED, bool MATPF>
 __device__ __forceinline__ void solve_instance(const KParams& p, int inst, double* v, double* scr,
                                                int lane) {
@@ -1399,12 +1408,11 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     if (can_check) chk_left = chk;
     const bool adapt = ar_int && --ar_left == 0;  // iter % ar_int == 0
     if (adapt) ar_left = ar_int;
-    // the larger buckets' check-time code gets an opaque copy of the lane id: its per-lane
-    // addresses are recomputed at each check instead of being hoisted out of the ADMM loop into
-    // registers (at RN = 4 the hoisted addresses spilled to scratch; at RN = 2 they fit in AGPRs
-    // and hoisting them measured faster)
+    // the check-time code gets an opaque copy of the lane id: its per-lane addresses are
+    // recomputed at each check instead of being hoisted out of the ADMM loop into registers (at
+    // RN = 4 the hoisted addresses spilled to scratch; MPCQP_OPAQUE_LANE_RN above)
     int clane = lane;
-    if constexpr (RN >= 4) asm volatile("" : "+v"(clane));
+    if constexpr (RN >= MPCQP_OPAQUE_LANE_RN) asm volatile("" : "+v"(clane));
 #ifndef MPCQP_FIXED_WORK
     if (can_check || adapt) {
       T_BEGIN(t_rs);
@@ -1560,10 +1568,10 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
       if (inst >= (unsigned int)p.B) continue;  // not a permutation entry: nothing to solve
     }
     if (p.skip && p.skip[inst]) continue;  // wave-uniform
-    // larger buckets: an opaque copy of the lane id per instance, so per-lane address arithmetic
-    // is not hoisted out of the instance loop (held in registers for the whole kernel it spills)
+    // an opaque copy of the lane id per instance, so per-lane address arithmetic is not hoisted
+    // out of the instance loop (MPCQP_OPAQUE_LANE_RN above)
     int ilane = lane;
-    if constexpr (RN >= 4) asm volatile("" : "+v"(ilane));
+    if constexpr (RN >= MPCQP_OPAQUE_LANE_RN) asm volatile("" : "+v"(ilane));
     solve_instance<RN, RM, PAIRED, MATPF>(p, (int)inst, v, scr, ilane);
     LDS_FENCE();
   }
