@@ -325,16 +325,18 @@ __device__ __forceinline__ void fac_step(const FacRec& r, double* v) {
 // Step loops.  Records (L2-resident, fixed stride) rotate through three register sets, so the
 // records of step s + 2 are in flight while steps s and s + 1 compute.  prefetch() issues the
 // first three steps' loads; callers issue it ahead of unrelated work to hide the L2 latency.
-template <typename Ops>
+// D = record sets in flight: 3 (records of step s + 2 load during step s) or 4 (s + 3; the
+// two-wave kernel's first wave, +0.7 % at N = 40 and -4.8 % in the one-wave N = 20 kernel)
+template <typename Ops, int D = 3>
 struct Pipe {
-  typename Ops::Rec a, b, c;
+  typename Ops::Rec a, b, c, d;  // d unused at D = 3
 };
 template <typename Ops>
 __device__ __forceinline__ int step_off(int n, int s) {
   return (s < n ? s : n - 1) * (Ops::STRIDE * 4);
 }
-template <typename Ops>
-__device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops>& p) {
+template <typename Ops, int D>
+__device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops, D>& p) {
   // n >= 1 (checked at plan time); no branch here, so the vmcnt bookkeeping after it is exact
   // the sets are issued in order (sched_barrier) so that the vmcnt wait for one set never
   // includes a later one
@@ -345,6 +347,10 @@ __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops
   __builtin_amdgcn_sched_barrier(0);
   Ops::load(rs, step_off<Ops>(n, 2), lane, p.c);
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (D == 4) {
+    Ops::load(rs, step_off<Ops>(n, 3), lane, p.d);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 // The rotation is unrolled 12 steps deep: LLVM's waitcnt insertion merges states pessimistically
 // at a loop header (the first step after it would wait for all three sets), so the header is
@@ -353,17 +359,25 @@ __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops
   ops.step(p.X, s);                                         \
   if (++s >= n) break;                                      \
   __builtin_amdgcn_sched_barrier(0);                        \
-  Ops::load(rs, step_off<Ops>(n, s + 2), lane, p.X);        \
+  Ops::load(rs, step_off<Ops>(n, s + D - 1), lane, p.X);    \
   __builtin_amdgcn_sched_barrier(0);
-template <typename Ops>
+template <typename Ops, int D>
 __device__ __forceinline__ void run_body(Rsrc rs, int n, uint32_t lane, const Ops& ops,
-                                         Pipe<Ops>& p) {
+                                         Pipe<Ops, D>& p) {
   int s = 0;
-  for (;;) {
-    MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
-    MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
-    MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
-    MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
+  if constexpr (D == 4) {
+    for (;;) {
+      MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c) MPCQP_STEP(d)
+      MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c) MPCQP_STEP(d)
+      MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c) MPCQP_STEP(d)
+    }
+  } else {
+    for (;;) {
+      MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
+      MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
+      MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
+      MPCQP_STEP(a) MPCQP_STEP(b) MPCQP_STEP(c)
+    }
   }
 }
 #undef MPCQP_STEP
@@ -442,8 +456,9 @@ struct FacOps {
   }
   __device__ __forceinline__ void step(const Rec& r, int) const { fac_step(r, v); }
 };
+template <int D = 3>
 __device__ __forceinline__ void run_fac(const uint32_t* tbl, int nsteps, double* v, int lane) {
-  Pipe<FacOps> pp;
+  Pipe<FacOps, D> pp;
   const Rsrc rs = table_rsrc(tbl, nsteps, FAC_STEP_WORDS);
   prefetch(rs, nsteps, (uint32_t)lane, pp);
   run_body(rs, nsteps, (uint32_t)lane, FacOps{v}, pp);
@@ -1586,6 +1601,11 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
 #endif
 }
 
+// record sets in flight of the two-wave kernel's first wave (Pipe; MPCQP_PAIR_PIPE=3 for A/B)
+#ifndef MPCQP_PAIR_PIPE
+#define MPCQP_PAIR_PIPE 4
+#endif
+constexpr int PAIR_PIPE = MPCQP_PAIR_PIPE;
 #include "engine_pair.inc"
 
 // ---------------------------------------------------------------------------------------- host
