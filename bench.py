@@ -15,10 +15,11 @@ in the timed region).
 
 Rank 0 prints one JSON line: metric/value/... + roofline (graded on the LDS, the resource the
 solve steps run on; HBM and FP64 fractions beside it) + cold (single-shot) rate + cpu_baseline
-+ three legs measured in the same run, each with its own roofline: config3 (N = 40 impulsive
++ four legs measured in the same run, each with its own roofline: config3 (N = 40 impulsive
 delta-v, BASELINE config 3) and n40_accel (N = 40 continuous acceleration, the horizon of every
-reference script), both at the headline's window, and config4 (the continuous-time nonlinear loop,
-BASELINE config 4, --cont-steps sample periods).  `value` counts the solves the engine ran: chasers that terminated
+reference script), both at the headline's window, config2 (BASELINE config 2: B = 1,024 at N = 20,
+one launch) and config4 (the continuous-time nonlinear loop, BASELINE config 4, --cont-steps
+sample periods).  `value` counts the solves the engine ran: chasers that terminated
 (reference src/trajectorySimulate.py:288-293) are skipped by the solver and not counted.
 """
 from __future__ import annotations
@@ -63,6 +64,21 @@ def lds_bytes_per_iter(nfwd, nbwd, n, m, atomics_per_step):
     need_n, need_m, need_k = -(-n // 64), -(-m // 64), (n + m) // 64 + 1
     slots = next(3 * b for b in (2, 4, 8) if need_n <= b and need_m <= 2 * b and 3 * b >= need_k)
     return (nfwd + nbwd) * 64 * (16 * 8 + atomics_per_step * 16) + 7 * slots * 512
+
+
+LDS_CLK_GHZ = 2.4          # the LDS array serves one cycle per clock per CU (MICROARCH, LDS)
+
+
+def lds_cycles_per_iter(nfwd, nbwd, n, m, atomics_per_step):
+    """LDS-array cycles one ADMM iteration occupies per wave, conflict-free (the planner's
+    lds_layout.cpp cost model floor, tests/test_schedule.py): a ds_read_b64 serves its two 32-lane
+    halves in 2 cycles, a ds_add_f64 (read-modify-write) its four 16-lane groups in 4 -- so the
+    atomics are priced at their real array cost, not as 16 bytes at the read rate -- and each
+    64-lane register slot of the vector passes costs 10 (rhs + C store, the D^-1 pass, the
+    read-back)."""
+    need_n, need_m, need_k = -(-n // 64), -(-m // 64), (n + m) // 64 + 1
+    slots = next(3 * b for b in (2, 4, 8) if need_n <= b and need_m <= 2 * b and 3 * b >= need_k)
+    return (nfwd + nbwd) * (16 * 2 + atomics_per_step * 4) + 10 * slots
 
 
 def flops_per_solve(iters, n, m, nnzA, nnzL, checks):
@@ -256,6 +272,8 @@ def roofline(run, S, K, elapsed):
     b_iter, b_fact, b_io = bytes_model(n, m, nnzA, nnzL)
     lds_iter = lds_bytes_per_iter(sched["fwd_steps"], sched["bwd_steps"], n, m,
                                   sched["atomics_per_step"])
+    cyc_iter = lds_cycles_per_iter(sched["fwd_steps"], sched["bwd_steps"], n, m,
+                                   sched["atomics_per_step"])
     itm = np.where(act, it, 0).astype(np.float64)
     chk = np.ceil(itm / 25.0)
     # per launch (shard j, step k): LDS bytes, flops, streaming-model bytes of its solved instances
@@ -270,6 +288,7 @@ def roofline(run, S, K, elapsed):
     # = all bytes of the timed region / its wall time (conservative: the gaps between launches
     # count too); the per-launch form (bytes of one launch / its HIP-event duration) beside it
     lds_ach = float(lds_b.sum() / elapsed) / 1e9
+    cyc_ach = float(itm.sum() * cyc_iter / elapsed) / 1e9  # LDS-array G cycles / s, chip-wide
     return dict(
         bound="lds", achieved=lds_ach, peak=LDS_PEAK_GBS, unit="GB/s", frac=lds_ach / LDS_PEAK_GBS,
         traffic=None, kernel=kernel_name(sched), kernel_ms_per_launch=float(np.mean(kt) * 1e3),
@@ -280,14 +299,21 @@ def roofline(run, S, K, elapsed):
         recompute="achieved = admm_iters_timed * lds_bytes_per_iter / (ms_per_step * steps / 1e3)",
         why="one QP per wave with the KKT factor and solve vector in LDS: the solve steps are LDS "
             "read/atomic passes; HBM carries only per-solve I/O and check reloads",
+        lds_array_cycles={
+            "achieved": cyc_ach, "peak": 256 * LDS_CLK_GHZ, "unit": "G LDS-array cycles/s",
+            "frac": cyc_ach / (256 * LDS_CLK_GHZ), "cycles_per_iter": cyc_iter,
+            "what": "atomic-aware LDS roof: the conflict-free array cycles of the solve steps and "
+                    "vector passes (ds_read_b64 2, ds_add_f64 4 per wave-instruction) over one "
+                    "cycle per clock per CU; the measured busy share incl. conflicts and the other "
+                    "phases is lds_busy"},
         fp64={"achieved": float(flops.sum() / elapsed) / 1e9, "peak": FP64_PEAK_GFLOPS,
               "unit": "GFLOP/s", "frac": float(flops.sum() / elapsed) / 1e9 / FP64_PEAK_GFLOPS},
-        streaming_model={"achieved": float(stream_b.sum() / elapsed) / 1e9, "unit": "GB/s",
-                         "frac_of_hbm_peak": float(stream_b.sum() / elapsed) / 1e9 / HBM_PEAK_GBS,
-                         "bytes_model": {"per_iter": b_iter, "per_factor": b_fact,
-                                         "per_solve_io": b_io},
-                         "note": "SURVEY 8(d) accounting (factor and iterates streamed every "
-                                 "iteration); they stay in LDS/VGPRs instead"})
+        survey_streaming_model={
+            "model_GBs_if_streamed": float(stream_b.sum() / elapsed) / 1e9,
+            "bytes_model": {"per_iter": b_iter, "per_factor": b_fact, "per_solve_io": b_io},
+            "note": "a MODEL, not a measurement: SURVEY 8(d)'s bytes if the factor and iterates "
+                    "were streamed from HBM every iteration; they stay in LDS / VGPRs, so no HBM "
+                    "fraction is claimed from it (the measured HBM figure is `hbm`)"})
 
 
 def attach_profiles(roof, B, nx, S, K, elapsed, dv=False):
@@ -417,13 +443,19 @@ def kernel_name(sched):
     return "qp_pair_kernel" if sched.get("waves_per_instance", 1) == 2 else "qp_batch_kernel"
 
 
-def lds_roof(iters_total, lds_iter, seconds, kernel_ms=None, fp64=None, kernel="qp_batch_kernel"):
+def lds_roof(iters_total, lds_iter, seconds, kernel_ms=None, fp64=None, kernel="qp_batch_kernel",
+             cyc_iter=None):
     """LDS-graded roofline of a leg: the LDS bytes its solve launches moved (ADMM iterations x
-    lds_bytes_per_iter) over the leg's timed wall time."""
+    lds_bytes_per_iter) over the leg's timed wall time (and the atomic-aware array-cycle roof)."""
     ach = iters_total * lds_iter / seconds / 1e9
     out = {"bound": "lds", "achieved": ach, "peak": LDS_PEAK_GBS, "unit": "GB/s",
            "frac": ach / LDS_PEAK_GBS, "traffic": None, "kernel": kernel,
            "lds_bytes_per_iter": lds_iter, "admm_iters_timed": float(iters_total)}
+    if cyc_iter is not None:
+        ca = iters_total * cyc_iter / seconds / 1e9
+        out["lds_array_cycles"] = {"achieved": ca, "peak": 256 * LDS_CLK_GHZ,
+                                   "unit": "G LDS-array cycles/s", "frac": ca / (256 * LDS_CLK_GHZ),
+                                   "cycles_per_iter": cyc_iter}
     if kernel_ms is not None:
         out["kernel_ms_per_launch"] = kernel_ms
     if fp64 is not None:
@@ -431,7 +463,7 @@ def lds_roof(iters_total, lds_iter, seconds, kernel_ms=None, fp64=None, kernel="
     return out
 
 
-def bench_leg(args, rank, device, nx, dv):
+def bench_leg(args, rank, device, nx, dv, batch=None, split=None, label=None):
     """A discrete closed-loop leg in the same run, at the headline's window (args.steps timed
     after args.warmup): N = 40 impulsive delta-v (BASELINE config 3, reference
     src/trajectorySimulate.py:110-111) and N = 40 continuous acceleration (the horizon every
@@ -440,7 +472,8 @@ def bench_leg(args, rank, device, nx, dv):
 
     sim, mpc, fail, deb = scenarios.radial_scenario(Nx=nx, isDeltaV=dv)
     prob = qp_model.build_problem(sim, mpc, fail, deb)
-    B, S = args.batch, max(1, min(args.split, args.batch))
+    B = batch or args.batch
+    S = max(1, min(split or args.split, B))
     K = args.leg_steps or args.steps
     W = args.leg_warmup if args.leg_warmup is not None else args.warmup
     X0 = initial_states(B, 0, B, args.seed)
@@ -453,7 +486,7 @@ def bench_leg(args, rank, device, nx, dv):
         c.close()
     model = "impulsive delta-v" if dv else "continuous acceleration"
     return {"metric": f"MPC-QP solves/sec @ N={nx}, {model}, CW, batch={B}; ADMM iters to "
-                      f"{args.eps:g}",
+                      f"{args.eps:g}" + (f" ({label})" if label else ""),
             "value": float(act.sum()) / run["elapsed"], "unit": "solves/s", "steps": K,
             "warmup": W, "ms_per_step": run["elapsed"] / K * 1e3,
             "config": {"workload": f"warm closed-loop MPC-QP solves, radial CW scenario, N=Nx={nx}, "
@@ -462,7 +495,8 @@ def bench_leg(args, rank, device, nx, dv):
                        "streams_per_gpu": S},
             "roofline": {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac",
                                               "traffic", "kernel", "kernel_ms_per_launch",
-                                              "lds_bytes_per_iter", "admm_iters_timed", "fp64")
+                                              "lds_bytes_per_iter", "admm_iters_timed", "fp64",
+                                              "lds_array_cycles", "hbm", "lds_busy")
                          if k in roof},
             "admm_iters": {"mean": float(it[act].mean()), "median": float(np.median(it[act])),
                            "p90": float(np.percentile(it[act], 90)), "max": int(it[act].max())},
@@ -537,7 +571,9 @@ def bench_continuous(args, rank, world, device, dist):
     # graded over the whole timed periods (plant + UKF + configure included); the solve launches
     # alone beside it (their HIP-event time)
     roof = lds_roof(it_timed, lds_iter, elapsed, kernel_ms=float(t_solve.mean()),
-                    kernel=kernel_name(sched))
+                    kernel=kernel_name(sched),
+                    cyc_iter=lds_cycles_per_iter(sched["fwd_steps"], sched["bwd_steps"], dims["n"],
+                                                 dims["m"], sched["atomics_per_step"]))
     roof["frac_over_solve_launches"] = it_timed * lds_iter / (t_solve.sum() * 1e-3) / 1e9 / LDS_PEAK_GBS
     return {
         "metric": f"MPC-QP solves/sec @ N={nx} offset-free MPC in the continuous-time nonlinear "
@@ -613,6 +649,11 @@ def main(argv=None):
                     out[key] = bench_leg(args, rank, device, nx, dv)
                 except Exception as e:  # report, never fake
                     out[key] = {"error": repr(e)}
+            try:  # BASELINE config 2: B = 1,024 at N = 20, one launch (latency-bound: one grid)
+                out["config2"] = bench_leg(args, rank, device, 20, False, batch=1024, split=1,
+                                           label="BASELINE config 2")
+            except Exception as e:  # report, never fake
+                out["config2"] = {"error": repr(e)}
             try:
                 ca = argparse.Namespace(**vars(args))
                 ca.nx, ca.dv, ca.steps, ca.warmup = 40, False, args.cont_steps, 1

@@ -170,6 +170,15 @@ int mpcqp_schedule_info(const mpcqp_handle *h, int32_t *fac_steps, int32_t *fwd_
  * solve step (3 for paired steps -- segments 0 + 1 of a lane summed into one target -- 4 otherwise).
  * The bench's LDS byte model reads it. */
 int mpcqp_schedule_kind(const mpcqp_handle *h, int32_t *atomics_per_step);
+/* The solve kernel the handle launches (any pointer may be NULL): *waves_per_instance (1, or 2 for
+ * the two-wave kernel), *instances_per_cu (resident instances per CU: LDS image and registers),
+ * *regs (registers per lane the kernel allocates, arch VGPRs + AGPRs, from hipFuncGetAttributes) and
+ * *scratch_bytes (per-lane scratch).  mpcqp_create refuses a kernel above the validated register /
+ * scratch budget (MPCQP_MAX_KERNEL_REGS / MPCQP_MAX_KERNEL_SCRATCH, DESIGN.md High-register builds). */
+#define MPCQP_MAX_KERNEL_REGS 440
+#define MPCQP_MAX_KERNEL_SCRATCH 512
+int mpcqp_kernel_info(const mpcqp_handle *h, int32_t *waves_per_instance, int32_t *instances_per_cu,
+                      int32_t *regs, int32_t *scratch_bytes);
 /* Which linear-system engine the handle runs (MPCQP_ENGINE_KKT: the only engine of this build;
  * round 1's dense-inverse alternative measured slower and was removed). */
 int mpcqp_engine_kind(const mpcqp_handle *h, int32_t *kind);

@@ -10,9 +10,11 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MPCQP_LIBRARY selects another build of the same ABI (diagnostic builds in tools/); there is no
-# fallback to anything else
-LIB_PATH = os.environ.get("MPCQP_LIBRARY") or os.path.join(_HERE, "libmpcqp.so")
+# MPCQP_LIBRARY selects another build of the same ABI (diagnostic builds in tools/), honoured only
+# together with MPCQP_DIAGNOSTICS=1 like every other MPCQP_* override (csrc/symbolic.hpp diag_env);
+# there is no fallback to anything else
+_DIAG = os.environ.get("MPCQP_DIAGNOSTICS") == "1"
+LIB_PATH = (_DIAG and os.environ.get("MPCQP_LIBRARY")) or os.path.join(_HERE, "libmpcqp.so")
 
 # every symbol include/mpcqp.h declares (checked by tests/test_abi.py)
 EXPORTED = (
@@ -21,6 +23,7 @@ EXPORTED = (
     "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_set_order", "mpcqp_get_state", "mpcqp_set_state", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
     "mpcqp_schedule_check",
     "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind", "mpcqp_schedule_kind",
+    "mpcqp_kernel_info",
     "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
     "mpcqp_cl_set_ids", "mpcqp_cl_set_tracking", "mpcqp_cl_noise", "mpcqp_cl_set_plant", "mpcqp_clc_period",
     "mpcqp_ukf_create", "mpcqp_ukf_destroy", "mpcqp_ukf_step", "mpcqp_plant_rk45",
@@ -102,51 +105,67 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise MPCQPError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
     L = C.CDLL(LIB_PATH)
+    # a host-only build (no HIP: the planner, the schedule interpreter and the settings/status entry
+    # points, for the sanitizer check of the host code, tests/test_sanitize.py) exports the marker
+    # mpcqp_host_only_build and nothing that touches a GPU; the product library must export all
+    host_only = hasattr(L, "mpcqp_host_only_build")
+
+    def _sig(L, name, what, value):
+        fn = getattr(L, name, None)
+        if fn is None:
+            if host_only:
+                return
+            raise MPCQPError(f"{LIB_PATH} does not export {name}")
+        setattr(fn, what, value)
+
     vp, i32, i32p, dp = C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.c_void_p
-    L.mpcqp_default_settings.argtypes = [C.POINTER(Settings)]
-    L.mpcqp_create.argtypes = [C.POINTER(Structure), C.POINTER(Settings), i32, vp,
-                               C.POINTER(vp)]
-    L.mpcqp_destroy.argtypes = [vp]
-    L.mpcqp_set_data.argtypes = [vp, dp, dp, dp, dp, dp]
-    L.mpcqp_update_bounds.argtypes = [vp, dp, dp]
-    L.mpcqp_update_A.argtypes = [vp, dp]
-    L.mpcqp_update_lin_cost.argtypes = [vp, dp]
-    L.mpcqp_warm_start.argtypes = [vp, dp, dp]
-    L.mpcqp_solve.argtypes = [vp, dp, dp, C.POINTER(Info)]
-    L.mpcqp_dims.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
-    L.mpcqp_engine_kind.argtypes = [vp, i32p]
-    L.mpcqp_schedule_kind.argtypes = [vp, i32p]
-    L.mpcqp_copy_data.argtypes = [vp, dp, dp, dp]
-    L.mpcqp_get_state.argtypes = [vp, dp, dp, dp, dp, dp]
-    L.mpcqp_set_state.argtypes = [vp, dp, dp, dp, dp, dp]
-    L.mpcqp_set_skip.argtypes = [vp, dp]
-    L.mpcqp_set_order.argtypes = [vp, dp]
-    L.mpcqp_data_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
-    L.mpcqp_schedule_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p]
-    L.mpcqp_export_symbolic.argtypes = [vp, i32p, i32p, i32p]
-    L.mpcqp_analyze.argtypes = [C.POINTER(Structure), i32p, i32p, i32p, i32p, i32p]
-    L.mpcqp_schedule_check.argtypes = [C.POINTER(Structure), dp, dp, C.c_double, dp, dp, dp,
-                                       C.POINTER(C.c_int64)]
-    L.mpcqp_cl_create.argtypes = [C.POINTER(ClScenario), i32, vp, C.POINTER(vp)]
-    L.mpcqp_cl_destroy.argtypes = [vp]
-    L.mpcqp_cl_configure.argtypes = [vp, dp, dp, dp, dp]
-    L.mpcqp_cl_step.argtypes = [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]
-    L.mpcqp_cl_set_ids.argtypes = [vp, C.c_int64]
-    L.mpcqp_cl_set_tracking.argtypes = [vp, dp, dp, dp, dp, C.c_double, C.c_double]
-    L.mpcqp_cl_noise.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_double, C.c_double, dp]
-    L.mpcqp_cl_set_plant.argtypes = [vp, C.POINTER(PlantModel), i32]
-    L.mpcqp_clc_period.argtypes = [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp,
-                                   dp, C.c_double, C.c_double, i32, i32, dp]
-    L.mpcqp_ukf_create.argtypes = [C.POINTER(UkfModel), i32, vp, C.POINTER(vp)]
-    L.mpcqp_ukf_destroy.argtypes = [vp]
-    L.mpcqp_ukf_step.argtypes = [vp, dp, dp, dp, dp, dp, dp]
-    L.mpcqp_plant_rk45.argtypes = [C.POINTER(PlantModel), i32, vp, dp, dp, dp, C.c_double,
-                                   C.c_double, i32, dp, dp]
-    L.mpcqp_status_string.argtypes = [i32]
-    L.mpcqp_status_string.restype = C.c_char_p
-    L.mpcqp_last_error.restype = C.c_char_p
+    _sig(L, "mpcqp_default_settings", "argtypes", [C.POINTER(Settings)])
+    _sig(L, "mpcqp_create", "argtypes", [C.POINTER(Structure), C.POINTER(Settings), i32, vp,
+                               C.POINTER(vp)])
+    _sig(L, "mpcqp_destroy", "argtypes", [vp])
+    _sig(L, "mpcqp_set_data", "argtypes", [vp, dp, dp, dp, dp, dp])
+    _sig(L, "mpcqp_update_bounds", "argtypes", [vp, dp, dp])
+    _sig(L, "mpcqp_update_A", "argtypes", [vp, dp])
+    _sig(L, "mpcqp_update_lin_cost", "argtypes", [vp, dp])
+    _sig(L, "mpcqp_warm_start", "argtypes", [vp, dp, dp])
+    _sig(L, "mpcqp_solve", "argtypes", [vp, dp, dp, C.POINTER(Info)])
+    _sig(L, "mpcqp_dims", "argtypes", [vp, i32p, i32p, i32p, i32p, i32p])
+    _sig(L, "mpcqp_engine_kind", "argtypes", [vp, i32p])
+    _sig(L, "mpcqp_schedule_kind", "argtypes", [vp, i32p])
+    _sig(L, "mpcqp_kernel_info", "argtypes", [vp, i32p, i32p, i32p, i32p])
+    _sig(L, "mpcqp_copy_data", "argtypes", [vp, dp, dp, dp])
+    _sig(L, "mpcqp_get_state", "argtypes", [vp, dp, dp, dp, dp, dp])
+    _sig(L, "mpcqp_set_state", "argtypes", [vp, dp, dp, dp, dp, dp])
+    _sig(L, "mpcqp_set_skip", "argtypes", [vp, dp])
+    _sig(L, "mpcqp_set_order", "argtypes", [vp, dp])
+    _sig(L, "mpcqp_data_buffers", "argtypes", [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)])
+    _sig(L, "mpcqp_schedule_info", "argtypes", [vp, i32p, i32p, i32p, i32p, i32p])
+    _sig(L, "mpcqp_export_symbolic", "argtypes", [vp, i32p, i32p, i32p])
+    _sig(L, "mpcqp_analyze", "argtypes", [C.POINTER(Structure), i32p, i32p, i32p, i32p, i32p])
+    _sig(L, "mpcqp_schedule_check", "argtypes", [C.POINTER(Structure), dp, dp, C.c_double, dp, dp, dp,
+                                       C.POINTER(C.c_int64)])
+    _sig(L, "mpcqp_cl_create", "argtypes", [C.POINTER(ClScenario), i32, vp, C.POINTER(vp)])
+    _sig(L, "mpcqp_cl_destroy", "argtypes", [vp])
+    _sig(L, "mpcqp_cl_configure", "argtypes", [vp, dp, dp, dp, dp])
+    _sig(L, "mpcqp_cl_step", "argtypes", [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp])
+    _sig(L, "mpcqp_cl_set_ids", "argtypes", [vp, C.c_int64])
+    _sig(L, "mpcqp_cl_set_tracking", "argtypes", [vp, dp, dp, dp, dp, C.c_double, C.c_double])
+    _sig(L, "mpcqp_cl_noise", "argtypes", [vp, C.c_uint64, C.c_uint64, C.c_double, C.c_double, dp])
+    _sig(L, "mpcqp_cl_set_plant", "argtypes", [vp, C.POINTER(PlantModel), i32])
+    _sig(L, "mpcqp_clc_period", "argtypes", [vp, dp, dp, i32, i32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp,
+                                   dp, C.c_double, C.c_double, i32, i32, dp])
+    _sig(L, "mpcqp_ukf_create", "argtypes", [C.POINTER(UkfModel), i32, vp, C.POINTER(vp)])
+    _sig(L, "mpcqp_ukf_destroy", "argtypes", [vp])
+    _sig(L, "mpcqp_ukf_step", "argtypes", [vp, dp, dp, dp, dp, dp, dp])
+    _sig(L, "mpcqp_plant_rk45", "argtypes", [C.POINTER(PlantModel), i32, vp, dp, dp, dp, C.c_double,
+                                   C.c_double, i32, dp, dp])
+    _sig(L, "mpcqp_status_string", "argtypes", [i32])
+    _sig(L, "mpcqp_status_string", "restype", C.c_char_p)
+    _sig(L, "mpcqp_last_error", "restype", C.c_char_p)
     for name in EXPORTED:
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None:
+            continue  # host-only diagnostics build (checked by _sig)
         if name not in ("mpcqp_status_string", "mpcqp_last_error"):
             fn.restype = C.c_int
     _lib = L

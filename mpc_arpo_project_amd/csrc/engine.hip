@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/mpcqp.h"
+#include "host_abi.hpp"
 #include "symbolic.hpp"
 
 using namespace mpcqp;
@@ -53,6 +54,9 @@ struct EllDev {
 struct DevPlan {
   EllDev eA, eAt, eP;  // residual mat-vecs (symbolic.hpp Ell)
   const uint32_t *fac, *tail, *fwd, *bwd;  // fixed-stride step records (symbolic.hpp)
+  // KM_MREG kernels: the solve records split into vector-operand + target records (fwdc, bwdc) and
+  // the matrix operands' LDS addresses (fwdm, bwdm), built on the host (mpcqp_create)
+  const uint32_t *fwdc, *bwdc, *fwdm, *bwdm;
   int nfac, ntail, nfwd, nbwd;
   const uint16_t* Lcol;    // DINV slot of each L entry's column
   int inst_doubles;        // LDS doubles of the instance image (16-byte aligned)
@@ -65,6 +69,7 @@ struct DevPlan {
   const uint32_t* bcopy;  // per lane: diagonal-pass slots whose W starts at (1/D) W (Plan::bcopy)
   int S_ZERO;
   int MV, MVZ;  // resident scaled values [P | A] (CSC orders) and their zero slot
+  int mv_slab;  // doubles of the per-wave slab holding them instead (Plan::mv_global), else 0
   const uint16_t *sra, *sca;  // lane-major row / column scaling slots (symbolic.hpp Plan::sra)
   int SJ;
   int XCH, XID;  // two-wave kernel: exchange slots and the handed-over instance id (Plan::XCH)
@@ -437,6 +442,111 @@ __device__ __forceinline__ void run_body_pf(Rsrc rs, int n, uint32_t lane, doubl
 }
 #undef MPCQP_PFSTEP
 
+// ---- matrix operands in registers (kernel mode KM_MREG) -------------------------------------
+// Every solve term is (matrix value) x (vector entry); the matrix values (L, the block inverses and
+// couplings N | G | G', the ONE / MONE / ZERO constants) are constant between factorizations.  After
+// every factorization the matrix operand of every term of the (at most MREG_STEPS) forward and
+// backward steps is read once into registers (MatRegs, 96 doubles per lane), and a solve step then
+// issues only its 8 vector-entry reads: 16 -> 8 ds_read_b64 per step (tools/lds_probe.hip at four
+// waves per CU: 342 -> 258 cycles per wave-step).  The host splits each term into its vector
+// address (in W or C) and its matrix address (anything else) -- the product is commutative and
+// fma(-x1, y1, -(x0 y0)) does not depend on the operands' order, so the results are bit-identical
+// to the LDS-operand kernel on the same plan.
+constexpr int MREG_STEPS = 6;
+struct MatRegs {
+  double m[2][MREG_STEPS][SOLVE_MAXC];  // [forward / backward][step][term]
+};
+// compact step record: vector addresses of the 8 terms, then the 4 targets (3 rows of 64 lane quads)
+constexpr int SOLVEC_STEP_WORDS = 3 * 64 * 4;
+constexpr int SOLVEM_STEP_WORDS = 2 * 64 * 4;  // matrix addresses of the 8 terms (2 rows)
+struct SolveRecC {
+  uint32_t b[SOLVE_MAXC];
+  uint32_t t0, t1, t2, t3;
+};
+__device__ __forceinline__ void load_solve_c(Rsrc rs, int soff, uint32_t lane, SolveRecC& r) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + q * 1024, soff, 0);
+    r.b[4 * q] = w[0], r.b[4 * q + 1] = w[1], r.b[4 * q + 2] = w[2], r.b[4 * q + 3] = w[3];
+  }
+  const auto tg = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + 2048, soff, 0);
+  r.t0 = tg[0], r.t1 = tg[1], r.t2 = tg[2], r.t3 = tg[3];
+}
+// the registers of one solve: matrix values of steps 0..MREG_STEPS-1 (steps past n re-read the last
+// one: never used)
+__device__ __forceinline__ void load_mats(const uint32_t* tbl, int n, uint32_t lane, const double* v,
+                                          double (&m)[MREG_STEPS][SOLVE_MAXC]) {
+  const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(tbl), (short)0,
+                                                    n * SOLVEM_STEP_WORDS * 4, 0x00020000);
+#pragma unroll
+  for (int st = 0; st < MREG_STEPS; ++st) {
+    const int soff = (st < n ? st : n - 1) * (SOLVEM_STEP_WORDS * 4);
+    uint32_t a[SOLVE_MAXC];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u) + q * 1024, soff, 0);
+      a[4 * q] = w[0], a[4 * q + 1] = w[1], a[4 * q + 2] = w[2], a[4 * q + 3] = w[3];
+    }
+#pragma unroll
+    for (int c = 0; c < SOLVE_MAXC; ++c) m[st][c] = lds_ld(v, a[c]);
+  }
+}
+template <bool PAIRED>
+__device__ __forceinline__ void solve_step_r(const SolveRecC& r, const double (&x)[SOLVE_MAXC],
+                                             double* v) {
+  double y[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) y[c] = lds_ld(v, r.b[c]);
+  __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+  __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+  const double n0 = fma(-x[1], y[1], -(x[0] * y[0]));
+  const double n1 = fma(-x[3], y[3], -(x[2] * y[2]));
+  const double n2 = fma(-x[5], y[5], -(x[4] * y[4]));
+  const double n3 = fma(-x[7], y[7], -(x[6] * y[6]));
+  if constexpr (PAIRED) {
+    lds_add(r.t0, n0 + n1);
+  } else {
+    lds_add(r.t0, n0);
+    lds_add(r.t1, n1);
+  }
+  lds_add(r.t2, n2);
+  lds_add(r.t3, n3);
+  LDS_FENCE();
+}
+struct PipeC {
+  SolveRecC a, b, c;
+};
+__device__ __forceinline__ int step_off_c(int n, int s) {
+  return (s < n ? s : n - 1) * (SOLVEC_STEP_WORDS * 4);
+}
+__device__ __forceinline__ void prefetch_c(Rsrc rs, int n, uint32_t lane, PipeC& p) {
+  __builtin_amdgcn_sched_barrier(0);
+  load_solve_c(rs, step_off_c(n, 0), lane, p.a);
+  __builtin_amdgcn_sched_barrier(0);
+  load_solve_c(rs, step_off_c(n, 1), lane, p.b);
+  __builtin_amdgcn_sched_barrier(0);
+  load_solve_c(rs, step_off_c(n, 2), lane, p.c);
+  __builtin_amdgcn_sched_barrier(0);
+}
+// n <= MREG_STEPS (checked at create time): the unrolled positions index the matrix registers
+#define MPCQP_RSTEP(X, POS)                                 \
+  solve_step_r<PAIRED>(p.X, m[POS], v);                     \
+  if (++s >= n) break;                                      \
+  __builtin_amdgcn_sched_barrier(0);                        \
+  load_solve_c(rs, step_off_c(n, s + 2), lane, p.X);        \
+  __builtin_amdgcn_sched_barrier(0);
+template <bool PAIRED>
+__device__ __forceinline__ void run_body_r(Rsrc rs, int n, uint32_t lane, double* v, PipeC& p,
+                                           const double (&m)[MREG_STEPS][SOLVE_MAXC]) {
+  int s = 0;
+  for (;;) {
+    MPCQP_RSTEP(a, 0) MPCQP_RSTEP(b, 1) MPCQP_RSTEP(c, 2)
+    MPCQP_RSTEP(a, 3) MPCQP_RSTEP(b, 4) MPCQP_RSTEP(c, 5)
+    break;
+  }
+}
+#undef MPCQP_RSTEP
+
 template <bool PAIRED>
 struct SolveOps {
   typedef SolveRec Rec;
@@ -493,17 +603,20 @@ struct Inst {
 };
 
 // per-wave scratch slab (doubles): the scalings D, E of the wave's current instance (the
-// infeasibility certificates and the unscaling of the solution).  The scaled matrix values stay
-// in LDS (Plan::MV).
+// infeasibility certificates and the unscaling of the solution), then -- with Plan::mv_global --
+// the scaled matrix values [P | A] (MV-relative indices; otherwise they stay in LDS, Plan::MV).
 struct Slab {
-  double *D, *E;
+  double *D, *E, *MV;
 };
-__host__ __device__ __forceinline__ size_t slab_doubles(int n, int m) { return (size_t)n + m; }
-__device__ __forceinline__ size_t slab_doubles(const DevPlan& P) { return slab_doubles(P.n, P.m); }
+__host__ __device__ __forceinline__ size_t slab_doubles(int n, int m, int mv_slab) {
+  return (((size_t)n + m + 1) & ~size_t(1)) + mv_slab;
+}
+__device__ __forceinline__ size_t slab_doubles(const DevPlan& P) { return slab_doubles(P.n, P.m, P.mv_slab); }
 __device__ __forceinline__ Slab slab_of(const DevPlan& P, double* scr) {
   Slab s;
   s.D = scr;
   s.E = s.D + P.n;
+  s.MV = scr + ((P.n + P.m + 1) & ~1);  // 16-byte aligned (the slab base is)
   return s;
 }
 // residual mat-vec out[r] = sum_k v[vpos[t]] * in[in_idx[t]], t = off_r + 64 k + lane, for every
@@ -540,8 +653,10 @@ __device__ __forceinline__ void ell_load(const EllDev& e, EllTk<R, KMAX>& t, int
     }
   }
 }
+// mv: the resident scaled values -- the LDS image (Plan::MV slots) or the wave's slab
+// (Plan::mv_global, MV-relative); in: the input vector staged in LDS
 template <int R, int KMAX>
-__device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>& t, const double* v,
+__device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>& t, const double* mv,
                                           const double* in, double (&out)[R], int lane) {
   constexpr int LPF = ELL_LPF;
   const uint32_t(&lp)[LPF] = t.lp;
@@ -552,7 +667,7 @@ __device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>&
     if (e.K[r] != 0) {
       double a[KMAX], b[KMAX];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) a[k] = v[t.tk[r][k] & 0xffffu], b[k] = in[t.tk[r][k] >> 16];
+      for (int k = 0; k < KMAX; ++k) a[k] = mv[t.tk[r][k] & 0xffffu], b[k] = in[t.tk[r][k] >> 16];
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) s += a[k] * b[k];
     }
@@ -565,12 +680,12 @@ __device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>&
 #pragma unroll
     for (int k = 0; k < LPF; ++k)
       if (k == L) {
-        if (lane < e.long_cnt[L]) s += v[lp[k]] * in[li[k]];
+        if (lane < e.long_cnt[L]) s += mv[lp[k]] * in[li[k]];
         t0 = lane + 64;
       }
     for (int t = t0; t < e.long_cnt[L]; t += 64) {
       const int q = e.long_off[L] + t;
-      s += v[e.vpos[q]] * in[e.in[q]];
+      s += mv[e.vpos[q]] * in[e.in[q]];
     }
     s = wave_sum(s);
     const int o = e.long_out[L];
@@ -580,11 +695,11 @@ __device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>&
   }
 }
 template <int R, int KMAX>
-__device__ __forceinline__ void ell_mv(const EllDev& e, const double* v, const double* in,
+__device__ __forceinline__ void ell_mv(const EllDev& e, const double* mv, const double* in,
                                        double (&out)[R], int lane) {
   EllTk<R, KMAX> t;
   ell_load(e, t, lane);
-  ell_apply(e, t, v, in, out, lane);
+  ell_apply(e, t, mv, in, out, lane);
 }
 // The Ruiz passes' index lists, loaded once per solve into registers (lane-major, 8 bytes = four
 // u16 slots per load; shared by every instance: L1/L2 hits): the passes then read only values.
@@ -726,8 +841,8 @@ struct Resid {
 // KKT values [[P + sigma I, A'], [A, -diag(1/rho)]] into the permuted LDS image
 // (OSQP kkt.c form_KKT / update_KKT_*), then factorize.
 template <int RN, int RM>
-__device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab& sb, double* v, int lane,
-                                    const Inst<RN, RM>& S) {
+__device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab& sb, double* v,
+                                                    const double* mv, int lane, const Inst<RN, RM>& S) {
   const DevPlan& P = p.pl;
   for (int k = lane; k < P.nnzL; k += 64) v[P.LX + k] = 0.0;
   // the whole 1/D region (the D_j tasks' KKT diagonal in, 1/D_j out; 0 in the padding, which the
@@ -743,10 +858,10 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
   for (int j = lane; j < P.n; j += 64) v[P.slotSig[j]] = p.s.sigma;
   LDS_FENCE();
   for (int k = lane; k < P.nnzP; k += 64) {
-    const double val = v[P.MV + k];
+    const double val = mv[P.MV + k];
     v[P.slotP[k]] = (P.Pi[k] == P.Pcol[k]) ? val + p.s.sigma : val;
   }
-  for (int k = lane; k < P.nnzA; k += 64) v[P.slotA[k]] = v[P.MV + P.nnzP + k];
+  for (int k = lane; k < P.nnzA; k += 64) v[P.slotA[k]] = mv[P.MV + P.nnzP + k];
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
@@ -767,7 +882,7 @@ __device__ __forceinline__ void assemble_and_factor(const KParams& p, const Slab
 #endif
 template <int RN, int RM>
 __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>& S, Resid<RN, RM>& R,
-                                  const Slab& sb, double* v, int lane TACC_PARAM) {
+                                  const Slab& sb, double* v, const double* mv, int lane TACC_PARAM) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
   double* xb = v + P.W;
@@ -786,15 +901,15 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   double pr = 0.0, dr = 0.0;
   T_END(T_RS0, t_r0);
   T_BEGIN(t_r1);
-  ell_mv<RM, ELL_KA>(P.eA, v, xb, R.Ax, lane);  // padding terms are 0 * x
+  ell_mv<RM, ELL_KA>(P.eA, mv, xb, R.Ax, lane);  // padding terms are 0 * x
   TSYNC(R.Ax[0]);
   T_END(T_RS1, t_r1);
   T_BEGIN(t_r2);
-  ell_mv<RN, ELL_KP>(P.eP, v, xb, R.Px, lane);
+  ell_mv<RN, ELL_KP>(P.eP, mv, xb, R.Px, lane);
   TSYNC(R.Px[0]);
   T_END(T_RS2, t_r2);
   T_BEGIN(t_r3);
-  ell_mv<RN, ELL_KAT>(P.eAt, v, yb, R.Aty, lane);
+  ell_mv<RN, ELL_KAT>(P.eAt, mv, yb, R.Aty, lane);
   TSYNC(R.Aty[0]);
   T_END(T_RS3, t_r3);
   T_BEGIN(t_r4);
@@ -818,8 +933,8 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
 
 template <int RN, int RM>
 __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, RM>& S, double (&dy)[RM],
-                                     const Slab& sb, const double (&Ev)[RM], double* v, int lane,
-                                     double eps) {
+                                     const Slab& sb, const double (&Ev)[RM], double* v,
+                                     const double* mv, int lane, double eps) {
   const DevPlan& P = p.pl;
   const double thr = OSQP_INFTY * MIN_SCALING;
   double nrm = 0.0;
@@ -851,7 +966,7 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
   LDS_FENCE();
   // A' dy by the residual ELL (same term order as the CSC column traversal, loads batched)
   double aty[RN];
-  ell_mv<RN, ELL_KAT>(P.eAt, v, yb, aty, lane);
+  ell_mv<RN, ELL_KAT>(P.eAt, mv, yb, aty, lane);
   double mx = 0.0;
 #pragma unroll
   for (int r = 0; r < RN; ++r)
@@ -862,8 +977,8 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
 
 template <int RN, int RM>
 __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM>& S, const double (&dx)[RN],
-                                   const Slab& sb, const double (&Dv)[RN], double* v, int lane,
-                                   double eps) {
+                                   const Slab& sb, const double (&Dv)[RN], double* v,
+                                   const double* mv, int lane, double eps) {
   const DevPlan& P = p.pl;
   const double thr = OSQP_INFTY * MIN_SCALING;
   double nrm = 0.0, qdx = 0.0;
@@ -886,7 +1001,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
   LDS_FENCE();
   // P dx and A dx by the residual ELLs (same term orders as the symmetric / CSR traversals)
   double pdx[RN];
-  ell_mv<RN, ELL_KP>(P.eP, v, xb, pdx, lane);
+  ell_mv<RN, ELL_KP>(P.eP, mv, xb, pdx, lane);
   double mx = 0.0;
 #pragma unroll
   for (int r = 0; r < RN; ++r)
@@ -894,7 +1009,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
   mx = wave_max(mx);
   if (!(mx < S.c * eps * nrm)) return false;
   double adx[RM];
-  ell_mv<RM, ELL_KA>(P.eA, v, xb, adx, lane);
+  ell_mv<RM, ELL_KA>(P.eA, mv, xb, adx, lane);
   int bad = 0;
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
@@ -909,7 +1024,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
 template <int RN, int RM>
 __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>& S, const Resid<RN, RM>& R,
                                  double (&dy)[RM], const double (&dx)[RN], const Slab& sb,
-                                 double* v, int lane, bool approximate TACC_PARAM) {
+                                 double* v, const double* mv, int lane, bool approximate TACC_PARAM) {
   T_BEGIN(t_m0);
   const DevPlan& P = p.pl;
   // the scalings D, E of the infeasibility certificates: loaded first, in flight under the norms
@@ -959,13 +1074,13 @@ __device__ __forceinline__ int check_termination(const KParams& p, Inst<RN, RM>&
   if (S.pri_res < eps_prim)
     prim_ok = true;
   else
-    prim_inf = is_primal_infeasible(p, S, dy, sb, Ev, v, lane, eps_pinf);
+    prim_inf = is_primal_infeasible(p, S, dy, sb, Ev, v, mv, lane, eps_pinf);
   T_END(T_TM1, t_m1);
   T_BEGIN(t_m2);
   if (S.dua_res < eps_dual)
     dual_ok = true;
   else
-    dual_inf = is_dual_infeasible(p, S, dx, sb, Dv, v, lane, eps_dinf);
+    dual_inf = is_dual_infeasible(p, S, dx, sb, Dv, v, mv, lane, eps_dinf);
   T_END(T_TM2, t_m2);
   if (prim_ok && dual_ok) return approximate ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED;
   if (prim_inf) return approximate ? MPCQP_PRIMAL_INFEASIBLE_INACCURATE : MPCQP_PRIMAL_INFEASIBLE;
@@ -1135,8 +1250,8 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
 // (read from there by the residual mat-vecs, certificates, KKT (re)assembly and the objective)
 template <int RN, int RM>
 __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs, Inst<RN, RM>& S,
-                                             const Slab& sb, double* v, int lane, const double (&D)[RN],
-                                             const double (&E)[RM]) {
+                                             const Slab& sb, double* v, double* mvw, int lane,
+                                             const double (&D)[RN], const double (&E)[RM]) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
   S.cinv = 1. / S.c;
@@ -1180,12 +1295,15 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = k0 + 64 * u + lane;
-        if (k < cnt) v[P.MV + k] = x[u];
+        if (k < cnt) mvw[P.MV + k] = x[u];
       }
     }
-    if (lane == 0) v[P.MVZ] = 0.0;
+    if (lane == 0) mvw[P.MVZ] = 0.0;
   }
   LDS_FENCE();
+  // global slab copy (Plan::mv_global): other lanes read these values back -- the stores must be
+  // complete and visible to the wave's later loads (workgroup-scope release/acquire)
+  if (P.mv_slab) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 }
 
 // Register buckets from which the per-lane addresses get an opaque lane id per instance (and per
@@ -1197,12 +1315,18 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
 #ifndef MPCQP_OPAQUE_LANE_RN
 #define MPCQP_OPAQUE_LANE_RN 2
 #endif
-template <int RN, int RM, bool PAIRED, bool MATPF>
+// kernel modes of the one-wave kernel: KM_LDS the solve steps read both operands from LDS;
+// KM_MATPF matrix operands one step ahead (diagnostic, rejected); KM_MVG the resident scaled values
+// in the wave's global slab (Plan::mv_global); KM_MREG matrix operands in registers (MatRegs)
+enum { KM_LDS = 0, KM_MATPF = 1, KM_MVG = 2, KM_MREG = 3 };
+template <int RN, int RM, bool PAIRED, int KM>
 __device__ __forceinline__ void solve_instance(const KParams& p, int inst, double* v, double* scr,
                                                int lane) {
+  constexpr bool MATPF = KM == KM_MATPF, MVG = KM == KM_MVG, MREG = KM == KM_MREG;
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
   const Slab sb = slab_of(P, scr);
+  double* const mv = MVG ? sb.MV : v;
   Inst<RN, RM> S;
   const int hs = p.has_state[inst];
 #ifdef MPCQP_TIMING
@@ -1213,16 +1337,22 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     double D[RN], E[RM];
     scale_problem<RN, RM>(p, inst, S, v, lane, D, E);
     T_BEGIN(t_sf);
-    scale_finish<RN, RM>(p, inst, hs, S, sb, v, lane, D, E);
+    scale_finish<RN, RM>(p, inst, hs, S, sb, v, mv, lane, D, E);
     T_END(T_SCFIN, t_sf);
   }
   T_END(T_SCALE, t_sc);
   S.rho = (hs != 0) ? p.rho_state[inst] : p.rho0;
   set_rho(S);
   T_BEGIN(t_f0);
+  MatRegs M;  // KM_MREG: the solve steps' matrix operands of the current factorization
 #ifndef MPCQP_ABL_NOFAC  // fixed-work ablation builds only
-  assemble_and_factor<RN, RM>(p, sb, v, lane, S);
+  assemble_and_factor<RN, RM>(p, sb, v, mv, lane, S);
 #endif
+  if constexpr (MREG) {
+    LDS_FENCE();
+    load_mats(P.fwdm, P.nfwd, (uint32_t)lane, v, M.m[0]);
+    load_mats(P.bwdm, P.nbwd, (uint32_t)lane, v, M.m[1]);
+  }
   T_END(T_FACTOR, t_f0);
   T_COUNT(T_NFACT);
 
@@ -1258,7 +1388,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       if (lane + 64 * r < n) xb[lane + 64 * r] = S.x[r];
     LDS_FENCE();
     double az[RM];
-    ell_mv<RM, ELL_KA>(P.eA, v, xb, az, lane);  // CSR row order
+    ell_mv<RM, ELL_KA>(P.eA, mv, xb, az, lane);  // CSR row order
 #pragma unroll
     for (int r = 0; r < RM; ++r) S.z[r] = lane + 64 * r < m ? az[r] : 0.0;
     LDS_FENCE();
@@ -1310,13 +1440,19 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   double dx[RN], dy[RM];
   Resid<RN, RM> R;
   Pipe<SolveOps<PAIRED>> sp;
+  PipeC spc;
   const SolveOps<PAIRED> sops{v};
-  const Rsrc rs_fwd = table_rsrc(P.fwd, P.nfwd, SOLVE_STEP_WORDS);
-  const Rsrc rs_bwd = table_rsrc(P.bwd, P.nbwd, SOLVE_STEP_WORDS);
+  const Rsrc rs_fwd = MREG ? table_rsrc(P.fwdc, P.nfwd, SOLVEC_STEP_WORDS)
+                           : table_rsrc(P.fwd, P.nfwd, SOLVE_STEP_WORDS);
+  const Rsrc rs_bwd = MREG ? table_rsrc(P.bwdc, P.nbwd, SOLVEC_STEP_WORDS)
+                           : table_rsrc(P.bwd, P.nbwd, SOLVE_STEP_WORDS);
   for (iter = 1; iter <= p.s.max_iter; ++iter) {
     T_COUNT(T_ITERS);
     T_BEGIN(t_v0);
-    prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);  // lands while the right-hand side is formed
+    if constexpr (MREG)  // lands while the right-hand side is formed
+      prefetch_c(rs_fwd, P.nfwd, (uint32_t)lane, spc);
+    else
+      prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);
     double xp[RN], zp[RM], bz[RM];
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
     // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
@@ -1345,14 +1481,19 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     T_END(T_V0, t_v0);
     T_BEGIN(t_fw);
 #ifndef MPCQP_ABL_NOSOLVE
-    if constexpr (MATPF)
+    if constexpr (MREG)
+      run_body_r<PAIRED>(rs_fwd, P.nfwd, (uint32_t)lane, v, spc, M.m[0]);
+    else if constexpr (MATPF)
       run_body_pf<PAIRED>(rs_fwd, P.nfwd, (uint32_t)lane, v, sp);
     else
       run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
 #endif
     T_END(T_FWD, t_fw);
     T_BEGIN(t_v1);
-    prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);  // lands during the diagonal pass
+    if constexpr (MREG)  // lands during the diagonal pass
+      prefetch_c(rs_bwd, P.nbwd, (uint32_t)lane, spc);
+    else
+      prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);
 #ifndef MPCQP_ABL_NODIAG
     {
       // C = (1/D) W; W restarts at 0, or at C where the row's identity term is folded into it
@@ -1376,7 +1517,9 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     T_END(T_V1, t_v1);
     T_BEGIN(t_bw);
 #ifndef MPCQP_ABL_NOSOLVE
-    if constexpr (MATPF)
+    if constexpr (MREG)
+      run_body_r<PAIRED>(rs_bwd, P.nbwd, (uint32_t)lane, v, spc, M.m[1]);
+    else if constexpr (MATPF)
       run_body_pf<PAIRED>(rs_bwd, P.nbwd, (uint32_t)lane, v, sp);
     else
       run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
@@ -1431,7 +1574,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #ifndef MPCQP_FIXED_WORK
     if (can_check || adapt) {
       T_BEGIN(t_rs);
-      compute_residuals(p, S, R, sb, v, clane TACC_ARG);
+      compute_residuals(p, S, R, sb, v, mv, clane TACC_ARG);
       T_END(T_RESID, t_rs);
       T_COUNT(T_NCHK);
     }
@@ -1442,7 +1585,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       continue;
 #endif
       T_BEGIN(t_tm);
-      status = check_termination(p, S, R, dy, dx, sb, v, clane, false TACC_ARG);
+      status = check_termination(p, S, R, dy, dx, sb, v, mv, clane, false TACC_ARG);
       T_END(T_TERM, t_tm);
       if (status != 0) break;
       status = MPCQP_UNSOLVED;
@@ -1457,7 +1600,12 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         rho_updates++;
         LDS_FENCE();
         T_BEGIN(t_f1);
-        assemble_and_factor<RN, RM>(p, sb, v, clane, S);
+        assemble_and_factor<RN, RM>(p, sb, v, mv, clane, S);
+        if constexpr (MREG) {
+          LDS_FENCE();
+          load_mats(P.fwdm, P.nfwd, (uint32_t)clane, v, M.m[0]);
+          load_mats(P.bwdm, P.nbwd, (uint32_t)clane, v, M.m[1]);
+        }
 #ifdef MPCQP_TIMING
         const unsigned long long dt_f1 = __builtin_amdgcn_s_memtime() - t_f1;
         tacc[T_FACTOR] += dt_f1;
@@ -1473,13 +1621,13 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   T_BEGIN(t_tl);
   if (!can_check) {
     iter = iter - 1;
-    compute_residuals(p, S, R, sb, v, lane TACC_ARG);
-    status = check_termination(p, S, R, dy, dx, sb, v, lane, false TACC_ARG);
+    compute_residuals(p, S, R, sb, v, mv, lane TACC_ARG);
+    status = check_termination(p, S, R, dy, dx, sb, v, mv, lane, false TACC_ARG);
     if (status == 0) status = MPCQP_UNSOLVED;
   }
   if (iter > p.s.max_iter) iter = p.s.max_iter;
   if (status == MPCQP_UNSOLVED) {
-    const int st = check_termination(p, S, R, dy, dx, sb, v, lane, true TACC_ARG);
+    const int st = check_termination(p, S, R, dy, dx, sb, v, mv, lane, true TACC_ARG);
     status = st ? st : MPCQP_MAX_ITER_REACHED;
   }
 
@@ -1496,7 +1644,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     double part = 0.0;
     for (int k = lane; k < P.nnzP; k += 64) {
       const int i = P.Pi[k], j = P.Pcol[k];
-      const double pk = v[P.MV + k];
+      const double pk = mv[P.MV + k];
       part += (i == j) ? .5 * pk * xb[i] * xb[i] : pk * xb[i] * xb[j];
     }
 #pragma unroll
@@ -1548,12 +1696,13 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 
 // One wave per workgroup; the instance image is the workgroup's whole (dynamic) LDS, at address 0.
 // MPCQP_WAVES_PER_EU: minimum waves per SIMD the register allocation must allow (1: up to 512
-// VGPRs + AGPRs per lane; 2: at most 256)
+// VGPRs + AGPRs per lane; 2: at most 256).  The MVG build (resident values in the global slab, 5
+// instances per CU at N = 20) always allows two: one SIMD of the CU then runs two of the waves.
 #ifndef MPCQP_WAVES_PER_EU
 #define MPCQP_WAVES_PER_EU 1
 #endif
-template <int RN, int RM, bool PAIRED, bool MATPF>
-__global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParams p) {
+template <int RN, int RM, bool PAIRED, int KM>
+__global__ void __launch_bounds__(64, KM == KM_MVG ? 2 : MPCQP_WAVES_PER_EU) qp_batch_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = (int)threadIdx.x;
   if ((uint32_t)(uintptr_t)lds != 0u) __builtin_trap();  // schedule byte addresses assume base 0
@@ -1587,7 +1736,7 @@ __global__ void __launch_bounds__(64, MPCQP_WAVES_PER_EU) qp_batch_kernel(KParam
     // out of the instance loop (MPCQP_OPAQUE_LANE_RN above)
     int ilane = lane;
     if constexpr (RN >= MPCQP_OPAQUE_LANE_RN) asm volatile("" : "+v"(ilane));
-    solve_instance<RN, RM, PAIRED, MATPF>(p, (int)inst, v, scr, ilane);
+    solve_instance<RN, RM, PAIRED, KM>(p, (int)inst, v, scr, ilane);
     LDS_FENCE();
   }
 #ifdef MPCQP_PAD_AGPR
@@ -1609,11 +1758,7 @@ constexpr int PAIR_PIPE = MPCQP_PAIR_PIPE;
 #include "engine_pair.inc"
 
 // ---------------------------------------------------------------------------------------- host
-thread_local std::string g_err;
-int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
+int fail(int code, const std::string& msg) { return set_error(code, msg); }
 #define HIPCHK(x)                                                                   \
   do {                                                                              \
     hipError_t e_ = (x);                                                            \
@@ -1622,16 +1767,12 @@ int fail(int code, const std::string& msg) {
 
 typedef void (*kernel_fn)(KParams);
 
-// block caps of the blocked substitution (symbolic.hpp); MPCQP_CAPM / MPCQP_CAPW override them
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return (e && *e) ? atoi(e) : dflt;
-}
-int cap_m() { return env_int("MPCQP_CAPM", 0); }  // 0: chosen per structure
-int cap_w() { return env_int("MPCQP_CAPW", 0); }
+// block caps of the blocked substitution (symbolic.hpp); MPCQP_CAPM / MPCQP_CAPW override them.
+// Every MPCQP_* override below is a diagnostic: honoured only with MPCQP_DIAGNOSTICS=1 (diag_env)
+int env_int(const char* name, int dflt) { return diag_env_int(name, dflt); }
 
 template <int RN, int RM>
-kernel_fn pick(bool paired, int waves, bool matpf) {
+kernel_fn pick(bool paired, int waves, bool matpf, bool mvg, bool mreg) {
   // two waves, the solve steps on the first; MPCQP_W0DIAG=1: the diagonal pass too (mode 3,
   // measured equal to mode 2 at N = 40)
   if (waves == 3)
@@ -1643,45 +1784,72 @@ kernel_fn pick(bool paired, int waves, bool matpf) {
       return paired ? qp_pair_kernel<RN / 2, RM / 2, true, 1> : qp_pair_kernel<RN / 2, RM / 2, false, 1>;
     return paired ? qp_pair_kernel<RN / 2, RM / 2, true, 0> : qp_pair_kernel<RN / 2, RM / 2, false, 0>;
   }
+  if (mvg || mreg) {  // instantiated for the (2, 4) bucket only (the planner offers them there alone)
+    if constexpr (RN == 2) {
+      if (matpf || (mvg && mreg)) return nullptr;
+      if (mreg)
+        return paired ? qp_batch_kernel<RN, RM, true, KM_MREG> : qp_batch_kernel<RN, RM, false, KM_MREG>;
+      return paired ? qp_batch_kernel<RN, RM, true, KM_MVG> : qp_batch_kernel<RN, RM, false, KM_MVG>;
+    }
+    return nullptr;
+  }
   if (matpf)
-    return paired ? qp_batch_kernel<RN, RM, true, true> : qp_batch_kernel<RN, RM, false, true>;
-  return paired ? qp_batch_kernel<RN, RM, true, false> : qp_batch_kernel<RN, RM, false, false>;
+    return paired ? qp_batch_kernel<RN, RM, true, KM_MATPF> : qp_batch_kernel<RN, RM, false, KM_MATPF>;
+  return paired ? qp_batch_kernel<RN, RM, true, KM_LDS> : qp_batch_kernel<RN, RM, false, KM_LDS>;
 }
 
 // RN = ceil(n/64) and RM = ceil(m/64) rounded up to the instantiated buckets; the plan's step kind
 // and waves per instance
-kernel_fn select_kernel(int n, int m, bool paired, int waves, bool matpf) {
+kernel_fn select_kernel(int n, int m, bool paired, int waves, bool matpf, bool mvg, bool mreg) {
   int rn = 0, rm = 0;
   if (!kernel_bucket(n, m, rn, rm)) return nullptr;
-  if (rn == 2) return pick<2, 4>(paired, waves, matpf);
+  if (rn == 2) return pick<2, 4>(paired, waves, matpf, mvg, mreg);
 #ifndef MPCQP_ONLY_SMALL
-  if (rn == 4) return pick<4, 8>(paired, waves, matpf);
+  if (rn == 4) return pick<4, 8>(paired, waves, matpf, mvg, mreg);
 #endif
   return nullptr;
 }
 
-// waves per instance of the solve kernel (MPCQP_WAVES: 1; 2 = two waves, solve steps split
-// between them; 3 = two waves, solve steps on the first; unset or 0: chosen per structure by
-// auto_waves; DESIGN.md, Two waves per instance)
-int waves_per_instance() {
-  const int w = env_int("MPCQP_WAVES", 0);
-  return (w == 1 || w == 2 || w == 3) ? w : 0;
+// Matrix operands of the solve steps in registers (KM_MREG): one-wave plans of the (2, 4) bucket
+// whose forward and backward solves take at most MREG_STEPS steps each.  MPCQP_MREG=0/1 forces it
+// off / on (diagnostics).
+constexpr int MREG_DEFAULT = 0;
+bool use_mreg(const Plan& pl) {
+  int rn = 0, rm = 0;
+  const bool fits = pl.waves == 1 && !pl.mat_first && !pl.mv_global && pl.nfwd <= MREG_STEPS &&
+                    pl.nbwd <= MREG_STEPS && kernel_bucket(pl.n, pl.m, rn, rm) && rn == 2;
+  return fits && env_int("MPCQP_MREG", MREG_DEFAULT) != 0;
 }
-// The automatic choice: two waves per instance with the solve steps on the first (3) when the
-// one-wave image leaves at most two instances per CU -- then two of the CU's four SIMDs would idle,
-// and the second wave takes half of the vector passes, checks and Ruiz passes onto them (N = 40:
-// +8 % solves/s, profiles/r04/pair2); one wave otherwise (N = 20: four instances per CU, where the
-// second wave's barriers cost more than its share saves: -4 %)
-int auto_waves(const mpcqp_structure* st) {
-  Plan p1;
-  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, p1, cap_m(), cap_w(), 163840,
-                        4, 1, false))
-    return 1;
-  const int bytes = ((p1.LDS_N + 1) & ~1) * 8;
-  return 163840 / std::max(bytes, 1) <= 2 ? 3 : 1;
+// the KM_MREG record tables from the plan's solve records: per step, the terms' vector addresses
+// (the operand in the W or C region) + the targets (SolveRecC), and the terms' matrix addresses
+// (every other operand: L, N | G | G', ZERO / ONE / MONE); a padding term (both operands zero
+// slots) reads its matrix zero from the first and its vector zero from the second
+void split_records(const Plan& pl, const std::vector<uint32_t>& rec, int nsteps,
+                   std::vector<uint32_t>& vec, std::vector<uint32_t>& mat) {
+  auto is_vec = [&](uint32_t byte) {
+    const int d = (int)(byte / 8u);
+    return (d >= pl.W && d < pl.W + pl.NKP) || (d >= pl.CACC && d < pl.CACC + pl.NKP);
+  };
+  vec.assign((size_t)nsteps * SOLVEC_STEP_WORDS, 0u);
+  mat.assign((size_t)nsteps * SOLVEM_STEP_WORDS, 0u);
+  for (int st = 0; st < nsteps; ++st) {
+    const uint32_t* r = rec.data() + (size_t)st * SOLVE_STEP_WORDS;
+    uint32_t* cv = vec.data() + (size_t)st * SOLVEC_STEP_WORDS;
+    uint32_t* cm = mat.data() + (size_t)st * SOLVEM_STEP_WORDS;
+    for (int l = 0; l < 64; ++l) {
+      for (int c = 0; c < SOLVE_MAXC; ++c) {
+        // full record: row q = c / 2 holds lane quads (a_2q, b_2q, a_2q+1, b_2q+1)
+        const uint32_t a = r[(c / 2) * 256 + l * 4 + (c % 2) * 2];
+        const uint32_t b = r[(c / 2) * 256 + l * 4 + (c % 2) * 2 + 1];
+        const bool av = is_vec(a);
+        // compact rows: q = c / 4 holds lane quads of terms 4q..4q+3
+        cv[(c / 4) * 256 + l * 4 + (c % 4)] = av ? a : b;
+        cm[(c / 4) * 256 + l * 4 + (c % 4)] = av ? b : a;
+      }
+      for (int k = 0; k < 4; ++k) cv[2 * 256 + l * 4 + k] = r[SOLVE_TERM_WORDS + l * 4 + k];
+    }
+  }
 }
-// matrix operands of the solve steps read one step ahead (MPCQP_MATPF: 0 or 1; Plan::mat_first)
-bool matrix_prefetch() { return env_int("MPCQP_MATPF", 0) == 1; }
 
 template <typename T>
 size_t push_blob(std::vector<char>& blob, const std::vector<T>& v) {
@@ -1709,55 +1877,13 @@ struct mpcqp_handle {
   bool has_data = false;
   const int32_t* skip = nullptr;   // mpcqp_set_skip
   const int32_t* order = nullptr;  // mpcqp_set_order
-  int grid = 0, lds_bytes = 0, waves_per_cu = 0;
+  int grid = 0, lds_bytes = 0, waves_per_cu = 0, per_cu = 0;
+  int kregs = 0, kscratch = 0;  // the launched kernel's registers per lane and scratch bytes
   int block = 64;  // threads per workgroup: 64 per wave of an instance
   kernel_fn kern = nullptr;
 };
 
 extern "C" {
-
-int mpcqp_version(void) { return 100; }
-const char* mpcqp_last_error(void) { return g_err.c_str(); }
-
-const char* mpcqp_status_string(int32_t st) {
-  switch (st) {
-    case MPCQP_SOLVED: return "solved";
-    case MPCQP_SOLVED_INACCURATE: return "solved inaccurate";
-    case MPCQP_PRIMAL_INFEASIBLE_INACCURATE: return "primal infeasible inaccurate";
-    case MPCQP_DUAL_INFEASIBLE_INACCURATE: return "dual infeasible inaccurate";
-    case MPCQP_MAX_ITER_REACHED: return "maximum iterations reached";
-    case MPCQP_PRIMAL_INFEASIBLE: return "primal infeasible";
-    case MPCQP_DUAL_INFEASIBLE: return "dual infeasible";
-    case -5: return "interrupted";
-    case -6: return "run time limit reached";
-    case MPCQP_NON_CVX: return "problem non convex";
-    case MPCQP_UNSOLVED: return "unsolved";
-    default: return "unknown";
-  }
-}
-
-int mpcqp_default_settings(mpcqp_settings* s) {
-  if (!s) return fail(MPCQP_E_INVALID, "null settings");
-  s->rho = 0.1;
-  s->sigma = 1e-06;
-  s->alpha = 1.6;
-  s->eps_abs = 1e-3;
-  s->eps_rel = 1e-3;
-  s->eps_prim_inf = 1e-4;
-  s->eps_dual_inf = 1e-4;
-  s->delta = 1e-6;
-  s->adaptive_rho_tolerance = 5;
-  s->max_iter = 4000;
-  s->scaling = 10;
-  s->adaptive_rho = 1;
-  s->adaptive_rho_interval = 0;
-  s->polish = 0;
-  s->polish_refine_iter = 3;
-  s->check_termination = 25;
-  s->warm_start = 1;
-  s->scaled_termination = 0;
-  return 0;
-}
 
 int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t batch, void* stream,
                  mpcqp_handle** out) {
@@ -1774,10 +1900,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
   h->set = *s;
   h->B = batch;
   h->stream = (hipStream_t)stream;
-  int waves = waves_per_instance();
-  if (waves == 0) waves = auto_waves(st);
-  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, h->plan, cap_m(), cap_w(),
-                        163840, 4, waves, matrix_prefetch())) {
+  if (!plan_for(st, h->plan)) {
     std::string e = h->plan.error;
     delete h;
     return fail(MPCQP_E_UNSUPPORTED, e);
@@ -1797,8 +1920,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     return fail(code, msg);
   };
   {
+    const bool mreg = use_mreg(pl);
     h->kern = select_kernel(pl.n, pl.m, pl.paired,
-                            pl.waves == 2 ? (pl.split_steps ? 2 : 3) : 1, pl.mat_first);
+                            pl.waves == 2 ? (pl.split_steps ? 2 : 3) : 1, pl.mat_first, pl.mv_global,
+                            mreg);
     if (!h->kern) {
       delete h;
       return fail(MPCQP_E_UNSUPPORTED, "problem dimensions exceed the instantiated kernels");
@@ -1826,6 +1951,13 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
            o_ePq = push_blob(blob, pl.ellP.sk), o_sra = push_blob(blob, pl.sra),
            o_sca = push_blob(blob, pl.sca), o_wc = push_blob(blob, pl.wcopy),
            o_bc = push_blob(blob, pl.bcopy);
+    std::vector<uint32_t> fwdc, fwdm, bwdc, bwdm;
+    if (mreg) {
+      split_records(pl, pl.fwd, pl.nfwd, fwdc, fwdm);
+      split_records(pl, pl.bwd, pl.nbwd, bwdc, bwdm);
+    }
+    const size_t o_fwdc = push_blob(blob, fwdc), o_fwdm = push_blob(blob, fwdm),
+                 o_bwdc = push_blob(blob, bwdc), o_bwdm = push_blob(blob, bwdm);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
@@ -1835,6 +1967,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.fac = (const uint32_t*)(b + o_fac), dp.tail = (const uint32_t*)(b + o_tail);
     dp.fwd = (const uint32_t*)(b + o_fwd), dp.bwd = (const uint32_t*)(b + o_bwd);
     dp.nfac = pl.nfac, dp.ntail = pl.ntail, dp.nfwd = pl.nfwd, dp.nbwd = pl.nbwd;
+    dp.fwdc = (const uint32_t*)(b + o_fwdc), dp.fwdm = (const uint32_t*)(b + o_fwdm);
+    dp.bwdc = (const uint32_t*)(b + o_bwdc), dp.bwdm = (const uint32_t*)(b + o_bwdm);
     dp.Lcol = (const uint16_t*)(b + o_Lc);
     dp.slotP = (const uint16_t*)(b + o_sP), dp.slotA = (const uint16_t*)(b + o_sA);
     dp.slotRho = (const uint16_t*)(b + o_sR), dp.slotSig = (const uint16_t*)(b + o_sS);
@@ -1867,7 +2001,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     dp.ONE = pl.ONE, dp.MONE = pl.MONE, dp.LDS_N = pl.LDS_N, dp.NKS = pl.NKP / 64;
     dp.S_P = pl.S_P, dp.S_A = pl.S_A, dp.S_DT = pl.S_DT, dp.S_ET = pl.S_ET;
     dp.S_ZERO = pl.S_ZERO;
-    dp.MV = pl.MV, dp.MVZ = pl.MVZ;
+    dp.MV = pl.MV, dp.MVZ = pl.MVZ, dp.mv_slab = pl.mv_slab;
     dp.sra = (const uint16_t*)(b + o_sra), dp.sca = (const uint16_t*)(b + o_sca), dp.SJ = pl.SJ;
     dp.XCH = pl.XCH, dp.XID = pl.XID;
     // the vector passes address C through W's slot plus the compile-time distance 64 (RN + RM)
@@ -1890,10 +2024,25 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     if (hipFuncSetAttribute((const void*)h->kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             lds_cap) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipFuncSetAttribute");
+    // register / scratch guard: builds above ~440 registers computed wrong
+    // iterates from a wave's second instance on (High-register builds); a product kernel
+    // beyond the validated budget is refused instead of launched (diagnostic builds may raise it)
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, (const void*)h->kern) != hipSuccess)
+      return cleanup_fail(MPCQP_E_HIP, "hipFuncGetAttributes");
+    h->kregs = fa.numRegs;
+    h->kscratch = (int)fa.localSizeBytes;
+    if (h->kregs > env_int("MPCQP_REG_BUDGET", MPCQP_MAX_KERNEL_REGS) ||
+        h->kscratch > MPCQP_MAX_KERNEL_SCRATCH)
+      return cleanup_fail(MPCQP_E_UNSUPPORTED,
+                          "solve kernel allocates " + std::to_string(h->kregs) + " registers / " +
+                              std::to_string(h->kscratch) +
+                              " scratch bytes per lane: above the validated budget");
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)h->kern, h->block, lds_alloc) !=
             hipSuccess || nb <= 0)
       return cleanup_fail(MPCQP_E_UNSUPPORTED, "kernel does not fit on a CU (LDS/VGPR)");
+    h->per_cu = nb;
     h->waves_per_cu = nb * pl.waves;
     h->lds_bytes = lds_alloc;
     h->grid = std::min(batch, nb * ncu);
@@ -1910,7 +2059,7 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->Ecls, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
-            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid * slab_doubles(pl.n, pl.m)) ==
+            hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid * slab_doubles(pl.n, pl.m, pl.mv_slab)) ==
                 hipSuccess &&
             hipMalloc(&h->counter, 64) == hipSuccess;
   if (!ok) return cleanup_fail(MPCQP_E_HIP, "hipMalloc(batch buffers)");
@@ -2109,51 +2258,19 @@ int mpcqp_schedule_kind(const mpcqp_handle* h, int32_t* atomics_per_step) {
   return 0;
 }
 
+int mpcqp_kernel_info(const mpcqp_handle* h, int32_t* waves_per_instance, int32_t* instances_per_cu,
+                      int32_t* regs, int32_t* scratch_bytes) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  if (waves_per_instance) *waves_per_instance = h->plan.waves;
+  if (instances_per_cu) *instances_per_cu = h->per_cu;
+  if (regs) *regs = h->kregs;
+  if (scratch_bytes) *scratch_bytes = h->kscratch;
+  return 0;
+}
+
 int mpcqp_engine_kind(const mpcqp_handle* h, int32_t* kind) {
   if (!h || !kind) return fail(MPCQP_E_INVALID, "null argument");
   *kind = MPCQP_ENGINE_KKT;
-  return 0;
-}
-
-int mpcqp_analyze(const mpcqp_structure* st, int32_t* perm, int32_t* Lp, int32_t* Li,
-                  int32_t* nnzL, int32_t* stats) {
-  if (!st || !nnzL) return fail(MPCQP_E_INVALID, "null argument");
-  Plan pl;
-  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w(), 163840,
-                        4, waves_per_instance() ? waves_per_instance() : auto_waves(st),
-                        matrix_prefetch()))
-    return fail(MPCQP_E_UNSUPPORTED, pl.error);
-  const int cap = *nnzL;
-  *nnzL = pl.nnzL;
-  if (perm) std::copy(pl.perm.begin(), pl.perm.end(), perm);
-  if (Lp) std::copy(pl.Lp.begin(), pl.Lp.end(), Lp);
-  if (Li && cap >= pl.nnzL) std::copy(pl.Li.begin(), pl.Li.end(), Li);
-  if (stats) {
-    stats[0] = (int32_t)(pl.nfac + pl.ntail);
-    stats[1] = (int32_t)pl.nfwd;
-    stats[2] = (int32_t)pl.nbwd;
-    stats[3] = pl.levels_fwd;
-    stats[4] = pl.levels_bwd;
-    stats[5] = pl.LDS_N * (int)sizeof(double);
-  }
-  return 0;
-}
-
-int mpcqp_schedule_check(const mpcqp_structure* st, const double* Px, const double* Ax,
-                         double sigma, const double* rho_vec, const double* rhs, double* sol,
-                         int64_t* model) {
-  if (!st || !Px || !Ax || !rho_vec || !rhs || !sol) return fail(MPCQP_E_INVALID, "null argument");
-  Plan pl;  // the plan mpcqp_create would build (MPCQP_WAVES included)
-  if (!build_plan_tuned(st->n, st->m, st->Pp, st->Pi, st->Ap, st->Ai, pl, cap_m(), cap_w(), 163840,
-                        4, waves_per_instance() ? waves_per_instance() : auto_waves(st),
-                        matrix_prefetch()))
-    return fail(MPCQP_E_UNSUPPORTED, pl.error);
-  if (model) {
-    const LdsModel md = model_lds(pl);
-    model[0] = md.read, model[1] = md.atomic, model[2] = md.vec, model[3] = md.floor;
-  }
-  if (!emulate_kkt_solve(pl, Px, Ax, sigma, rho_vec, rhs, sol))
-    return fail(MPCQP_E_INVALID, "schedule emulation produced a non-finite or unzeroed slot, or changed a 1/D slot");
   return 0;
 }
 

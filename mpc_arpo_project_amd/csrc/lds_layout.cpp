@@ -35,7 +35,7 @@ namespace mpcqp {
 namespace {
 
 double envd(const char* k, double d) {
-  const char* e = getenv(k);
+  const char* e = diag_env(k);
   return (e && *e) ? atof(e) : d;
 }
 
@@ -225,7 +225,7 @@ struct Opt {
     };
     Step best = s;
     int bestc = cur;
-    const bool no_flip = pl.mat_first || getenv("MPCQP_NO_FLIP") != nullptr;
+    const bool no_flip = pl.mat_first || diag_env("MPCQP_NO_FLIP") != nullptr;
     for (int it = 0; it < moves; ++it) {
       if (cur < bestc) bestc = cur, best = s;
       const double T = T0 * std::pow(T1 / T0, (double)it / moves);
@@ -620,9 +620,9 @@ void optimize_lds(Plan& pl) {
   Opt o(pl);
   o.load();
   Rng rng(0x5eed);
-  const double scale = std::max(0.25, std::min(4.0, atof(getenv("MPCQP_ANNEAL_SCALE") ? getenv("MPCQP_ANNEAL_SCALE") : "1")));
+  const double scale = std::max(0.25, std::min(4.0, atof(diag_env("MPCQP_ANNEAL_SCALE") ? diag_env("MPCQP_ANNEAL_SCALE") : "1")));
   const long c0 = o.total();
-  const bool dbg = getenv("MPCQP_DUMP_CONFLICTS") != nullptr;
+  const bool dbg = diag_env("MPCQP_DUMP_CONFLICTS") != nullptr;
   for (int round = 0; round < 3; ++round) {
     for (Step& s : o.st) {
       const int b = dbg ? o.step_cost(s) : 0;
@@ -648,7 +648,7 @@ void optimize_lds(Plan& pl) {
       fprintf(stderr, "  step: %d used segs, %d targets, max segs/target %d, atomic excess %d\n", nu, nt, mx, ex);
     }
   }
-  if (getenv("MPCQP_DUMP_CONFLICTS")) fprintf(stderr, "optimize_lds: modelled cycles %ld -> %ld\n", c0, c1);
+  if (diag_env("MPCQP_DUMP_CONFLICTS")) fprintf(stderr, "optimize_lds: modelled cycles %ld -> %ld\n", c0, c1);
   o.store();
 }
 

@@ -275,7 +275,7 @@ int pack_solve_level_free(const std::vector<Task>& tasks, const Plan& pl, std::v
 }
 
 int pack_solve_level(const std::vector<Task>& tasks, const Plan& pl, std::vector<uint32_t>& tbl) {
-  if (getenv("MPCQP_DUMP_TASKS")) {
+  if (diag_env("MPCQP_DUMP_TASKS")) {
     fprintf(stderr, "level:");
     for (const Task& t : tasks) fprintf(stderr, " %c%zu", t.target >= pl.W && t.target < pl.W + pl.NKP ? 'w' : 'c', t.terms.size());
     fprintf(stderr, "\n");
@@ -763,7 +763,8 @@ std::vector<std::vector<Task>> place_accumulations(std::vector<std::vector<Task>
 }
 
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                const int32_t* Ai, Plan& pl, int capM, int capW, bool paired, int waves) {
+                const int32_t* Ai, Plan& pl, int capM, int capW, bool paired, int waves,
+                bool mv_global) {
   pl = Plan();
   pl.paired = paired;
   // waves: 1; 2 = two waves per instance, solve steps split between them; 3 = two waves per
@@ -1076,7 +1077,7 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   // the last backward level, 46.  That last level is the one that overflows one step (N = 20:
   // 360 segments), and folding it there brings the backward solve from 7 to 6 steps, so the
   // default (4) is: exact copy rows in both solves, the fold in the last backward level only.
-  const char* cr = getenv("MPCQP_COPY_ROWS");  // diagnostics: 0 block-0 copies, 1 copy rows only,
+  const char* cr = diag_env("MPCQP_COPY_ROWS");  // diagnostics: 0 block-0 copies, 1 copy rows only,
   const int copy_mode = cr ? atoi(cr) : 4;     // 2 fold everywhere, 3 fold backward, 4 default
   std::vector<uint8_t> fcopy(nk, 0), bcopy(nk, 0);
   for (int r = 0; r < nk; r++) {
@@ -1290,8 +1291,8 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   }
   pl.levels_fwd = T;
   pl.levels_bwd = T;
-  relocate(pl, !getenv("MPCQP_NO_LAYOUT"));
-  if (getenv("MPCQP_DUMP_CONFLICTS")) dump_conflicts(pl);
+  relocate(pl, !diag_env("MPCQP_NO_LAYOUT"));
+  if (diag_env("MPCQP_DUMP_CONFLICTS")) dump_conflicts(pl);
   if (pl.S_ET + m > pl.LDS_N) pl.LDS_N = pl.S_ET + m;  // the scaling value overlay
   pl.LDS_N = (pl.LDS_N + 1) & ~1;
 
@@ -1379,10 +1380,19 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     pl.S_ZERO = pl.S_ET + m;
     if (pl.S_ZERO + 1 > pl.LDS_N) pl.LDS_N = (pl.S_ZERO + 2) & ~1;
   }
-  // ---- resident scaled values (Plan::MV) behind the image; the ELL terms' LDS value slots
-  pl.MV = (pl.LDS_N + 1) & ~1;
-  pl.MVZ = pl.MV + pl.nnzP + pl.nnzA;
-  pl.LDS_N = (pl.MVZ + 2) & ~1;
+  // ---- resident scaled values (Plan::MV) behind the image, or in the wave's global slab
+  // (mv_global: one-wave plans only); the ELL terms' value slots
+  pl.mv_global = mv_global && pl.waves == 1;
+  if (pl.mv_global) {
+    pl.LDS_N = (pl.LDS_N + 1) & ~1;
+    pl.MV = 0;
+    pl.MVZ = pl.nnzP + pl.nnzA;
+    pl.mv_slab = (pl.MVZ + 2) & ~1;
+  } else {
+    pl.MV = (pl.LDS_N + 1) & ~1;
+    pl.MVZ = pl.MV + pl.nnzP + pl.nnzA;
+    pl.LDS_N = (pl.MVZ + 2) & ~1;
+  }
   if (pl.waves == 2) {  // the two-wave kernel's exchange slots and the handed-over instance id
     pl.XCH = pl.LDS_N;
     pl.XID = pl.XCH + XCH_DOUBLES;
@@ -1435,24 +1445,39 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
                       const int32_t* Ai, Plan& plan, int capM, int capW, int lds_per_cu,
                       int max_per_cu, int waves, bool mat_first) {
   // the LDS layout optimiser runs on the chosen plan (MPCQP_NO_ANNEAL=1: off, diagnostics)
-  const bool anneal = !getenv("MPCQP_NO_ANNEAL") && !getenv("MPCQP_NO_LAYOUT");
-  const char* fp = getenv("MPCQP_PAIRED");  // diagnostics: force the step kind
-  if (capM > 0 && capW > 0) {
-    if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW, !fp || atoi(fp) != 0, waves)) return false;
-    plan.mat_first = mat_first;
-    if (anneal) optimize_lds(plan);
-    finish_copy_masks(plan);
-    return true;
-  }
+  const bool anneal = !diag_env("MPCQP_NO_ANNEAL") && !diag_env("MPCQP_NO_LAYOUT");
+  const char* fp = diag_env("MPCQP_PAIRED");  // diagnostics: force the step kind
+  // diagnostics: MPCQP_MV=lds / global forces where the resident values live
+  const char* mvo = diag_env("MPCQP_MV");
+  const int mv_force = !mvo ? -1 : (strcmp(mvo, "global") == 0 ? 1 : 0);
+  // instances per CU of a plan built with the values in LDS, and -- only when forced
+  // (MPCQP_MV=global) -- with them moved to the global slab (one-wave (2, 4) plans, the kernel built
+  // for two waves per SIMD).  Measured at N = 20 (round 5): 5 instances per CU this way
+  // run 6 % SLOWER than 4 with the values in LDS (a fifth wave shares a SIMD: tools/lds_probe.hip
+  // puts a solve step at 880 cycles per wave with 5 waves per CU against 385 with 4), so the
+  // tuner does not pick it on its own
+  auto occupancy = [&](const Plan& p, bool& glob) {
+    const int lds = ((p.LDS_N + 1) & ~1) * 8;
+    int per_cu = std::min(max_per_cu, lds_per_cu / std::max(lds, 1));
+    glob = false;
+    if (p.waves == 1 && p.RN == 2 && mv_force == 1) {
+      const int pg = std::min(MV_GLOBAL_MAX_PER_CU, lds_per_cu / std::max(p.MV * 8, 1));
+      per_cu = std::max(per_cu, pg), glob = true;
+    }
+    return per_cu;
+  };
   if (n <= 0 || m < 0) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);
-  // structure key
+  const bool forced = capM > 0 && capW > 0;
+  // structure key (forced block caps included: diagnostics re-use their plans too)
   std::vector<int32_t> key;
   key.push_back(n), key.push_back(m), key.push_back(lds_per_cu), key.push_back(max_per_cu);
+  key.push_back(forced ? capM : 0), key.push_back(forced ? capW : 0);
   key.push_back(waves);
   key.push_back(mat_first);
   key.push_back(anneal);
   key.push_back(fp ? atoi(fp) : -1);
-  const char* cm = getenv("MPCQP_COPY_ROWS");  // diagnostics: the copy-row mode (build_plan)
+  key.push_back(mv_force);
+  const char* cm = diag_env("MPCQP_COPY_ROWS");  // diagnostics: the copy-row mode (build_plan)
   key.push_back(cm ? atoi(cm) : -1);
   key.insert(key.end(), Pp, Pp + n + 1);
   key.insert(key.end(), Pi, Pi + Pp[n]);
@@ -1468,6 +1493,19 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
       return true;
     }
   }
+  if (forced) {
+    bool glob = false;
+    if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW, !fp || atoi(fp) != 0, waves)) return false;
+    occupancy(plan, glob);
+    if (glob && !build_plan(n, m, Pp, Pi, Ap, Ai, plan, capM, capW, !fp || atoi(fp) != 0, waves, true))
+      return false;
+    plan.mat_first = mat_first;
+    if (anneal) optimize_lds(plan);
+    finish_copy_masks(plan);
+    std::lock_guard<std::mutex> g(mu);
+    memo[key] = plan;
+    return true;
+  }
   // Block caps stop at 192 and, among equally fast plans, the smallest blocks win: a block
   // inverse's entries grow with the block, and so does the rounding of the blocked substitution on
   // ill-conditioned (warm, large-rho) KKT systems -- at N = 20 a 192-row cap plan has the 176-row
@@ -1478,27 +1516,29 @@ bool build_plan_tuned(int n, int m, const int32_t* Pp, const int32_t* Pi, const 
   bool found = false;
   int best[5] = {0, 0, 0, 0, 0};  // -per_cu, step cost, block cap, fac steps, lds bytes
   int bm = 128, bw = 384;
-  bool bp = true;
+  bool bp = true, bg = false;
   for (int pk = 1; pk >= 0; --pk) {
     if (fp && atoi(fp) != pk) continue;
     for (int cm : CM)
       for (int cw : CW) {
         Plan pl;
         if (!build_plan(n, m, Pp, Pi, Ap, Ai, pl, cm, cw, pk != 0, waves)) continue;
-        const int lds = ((pl.LDS_N + 1) & ~1) * 8;
-        const int per_cu = std::min(max_per_cu, lds_per_cu / std::max(lds, 1));
+        bool glob = false;
+        const int per_cu = occupancy(pl, glob);
+        const int lds = glob ? pl.MV * 8 : ((pl.LDS_N + 1) & ~1) * 8;
         const int cost = (pl.nfwd + pl.nbwd) * (pk ? 92 : 100);
         const int sc[5] = {-per_cu, cost, cm, pl.nfac + pl.ntail, lds};
         if (!found || std::lexicographical_compare(sc, sc + 5, best, best + 5)) {
           found = true;
           std::copy(sc, sc + 5, best);
-          bm = cm, bw = cw, bp = pk != 0;
+          bm = cm, bw = cw, bp = pk != 0, bg = glob;
         }
       }
   }
   if (!found) return build_plan(n, m, Pp, Pi, Ap, Ai, plan);  // reports the error
-  if (getenv("MPCQP_DUMP_CAPS")) fprintf(stderr, "caps %d %d paired %d\n", bm, bw, (int)bp);
-  if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw, bp, waves)) return false;
+  if (diag_env("MPCQP_DUMP_CAPS"))
+    fprintf(stderr, "caps %d %d paired %d mv_global %d\n", bm, bw, (int)bp, (int)bg);
+  if (!build_plan(n, m, Pp, Pi, Ap, Ai, plan, bm, bw, bp, waves, bg)) return false;
   plan.mat_first = mat_first;
   if (anneal) optimize_lds(plan);
   finish_copy_masks(plan);

@@ -24,10 +24,27 @@
 // at the lane's sink slot.
 #pragma once
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
 namespace mpcqp {
+
+// Diagnostic environment switches (plan, layout, kernel-mode and occupancy overrides used by the
+// tools/ A/B scripts and a few white-box tests).  They are honoured ONLY when MPCQP_DIAGNOSTICS=1 is
+// set as well, so a product handle never picks up an unvalidated plan or kernel from an inherited
+// environment.  Returns null when the switch is off or the variable unset.
+inline const char* diag_env(const char* name) {
+  const char* on = getenv("MPCQP_DIAGNOSTICS");
+  if (!on || strcmp(on, "1") != 0) return nullptr;
+  const char* e = getenv(name);
+  return (e && *e) ? e : nullptr;
+}
+inline int diag_env_int(const char* name, int dflt) {
+  const char* e = diag_env(name);
+  return e ? atoi(e) : dflt;
+}
 
 constexpr int SOLVE_MAXC = 8;   // terms per lane of a solve step
 constexpr int FAC_MAXC = 4;     // terms per lane of a factorization step
@@ -138,6 +155,12 @@ struct Plan {
   // written at the end of the Ruiz scaling, read by the residual mat-vecs, the infeasibility
   // certificates, every (re)assembly of the KKT values and the objective; MVZ holds a zero
   int MV = 0, MVZ = 0;
+  // round 5: the resident values may instead live in the wave's global scratch slab (mv_global:
+  // MV = 0 and MVZ are then indices relative to the slab's value block of mv_slab doubles, and the
+  // LDS image ends before them) when that lets more instances share a CU (one-wave plans of the
+  // (2, 4) bucket: 5 per CU at N = 20, the kernel built for <= 256 registers; build_plan_tuned)
+  bool mv_global = false;
+  int mv_slab = 0;
   // the Ruiz rescale's row / column scaling slots of every value k = 64 j + l of [P | A] (CSC
   // orders; S_DT + i for P's rows, S_ET + i for A's, S_DT + j for columns) lane-major at [l][j],
   // j < SJ (a multiple of 4; padding -> 0), held in registers by the Ruiz passes
@@ -202,7 +225,12 @@ void finish_copy_masks(Plan& plan);
 // step, SOLVE_TERM_WORDS above) or with four independent segments (four atomics).
 bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                 const int32_t* Ai, Plan& plan, int capM = 128, int capW = 384, bool paired = true,
-                int waves = 1);
+                int waves = 1, bool mv_global = false);
+
+// instances per CU of the one-wave kernel with the resident values in global memory (its build for
+// two waves per SIMD: <= 256 registers, __launch_bounds__(64, 2)); the LDS-resident build stays at 4
+// (one wave per SIMD: up to 512 registers)
+constexpr int MV_GLOBAL_MAX_PER_CU = 5;
 
 // build_plan with the block caps and the step kind chosen per structure: over a grid of (capM <=
 // 192, capW) x {paired, unpaired}, the plan with the most instances per CU (LDS image within

@@ -277,13 +277,13 @@ class BatchQP:
         k, at = C.c_int32(), C.c_int32()
         check(_lib.lib().mpcqp_engine_kind(self._h, C.byref(k)), "mpcqp_engine_kind")
         check(_lib.lib().mpcqp_schedule_kind(self._h, C.byref(at)), "mpcqp_schedule_kind")
-        # instances per CU are set by the LDS image (160 KB per CU, at most 4 resident), so the
-        # waves per CU say how many waves one instance runs on (Two waves per instance)
-        per_cu = max(1, min(4, 163840 // max(1, v[3].value)))
+        w = [C.c_int32() for _ in range(4)]
+        check(_lib.lib().mpcqp_kernel_info(self._h, *[C.byref(x) for x in w]), "mpcqp_kernel_info")
         return dict(engine="kkt", fac_steps=v[0].value,
                     fwd_steps=v[1].value, bwd_steps=v[2].value, lds_bytes=v[3].value,
                     waves_per_cu=v[4].value, atomics_per_step=at.value,
-                    waves_per_instance=max(1, v[4].value // per_cu))
+                    waves_per_instance=w[0].value, instances_per_cu=w[1].value,
+                    kernel_regs=w[2].value, kernel_scratch_bytes=w[3].value)
 
     def dims(self):
         v = [C.c_int32() for _ in range(5)]

@@ -164,6 +164,27 @@ class Sweep:
         self.loop.close()
 
 
+def gather_traj(traj, G: int, rank: int, world: int, dist):
+    """the trajectories [hi - lo, steps + 1, 4] of every rank's contiguous shard gathered to rank 0
+    in global scenario order (a gather to rank 0, not an all-gather -- 1.2 GB per rank
+    at the config-5 size); uneven shards are padded to the largest one for the collective.
+    Returns the [G, steps + 1, 4] tensor on rank 0, None on the other ranks; `traj` itself without
+    a process group."""
+    import torch
+
+    if not dist:
+        return traj
+    per = -(-G // world)
+    pad = torch.zeros((per,) + tuple(traj.shape[1:]), dtype=traj.dtype, device=traj.device)
+    pad[:traj.shape[0]] = traj
+    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+    dist.gather(pad, bufs, dst=0)
+    if rank != 0:
+        return None
+    return torch.cat([bufs[r][:launch.shard_range(G, r, world)[1] - launch.shard_range(G, r, world)[0]]
+                      for r in range(world)])
+
+
 def reduce(S: np.ndarray):
     """headline statistics of a gathered [G, 9] summary (final error over completed runs)"""
     f = {k: S[:, i] for i, k in enumerate(FIELDS)}
@@ -318,19 +339,7 @@ def main(argv=None):
     el = _timed_run(sw, dist, device)
     local_sum = sw.summary()
     S = launch.gather_rows(local_sum, sw.G, rank, world, dist)
-    traj = None
-    if a.traj:
-        traj = sw.traj
-        if dist:  # to rank 0 only (a gather, not an all-gather, for 1.2 GB per rank)
-            per = -(-sw.G // world)
-            pad = torch.zeros(per, sw.nsim + 1, 4, dtype=torch.float64, device=device)
-            pad[:traj.shape[0]] = traj
-            bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
-            dist.gather(pad, bufs, dst=0)
-            if rank == 0:
-                traj = torch.cat([bufs[r][:launch.shard_range(sw.G, r, world)[1] -
-                                          launch.shard_range(sw.G, r, world)[0]]
-                                  for r in range(world)])
+    traj = gather_traj(sw.traj, sw.G, rank, world, dist) if a.traj else None
     if dist:
         t = torch.tensor([el], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -91,3 +91,17 @@ def test_horizon_limits():
         assert "too large" in str(e)
     else:
         raise AssertionError("Nx = 52 accepted")
+
+
+def test_plan_overrides_need_the_diagnostics_switch(prob20, monkeypatch):
+    """the MPCQP_* plan / kernel overrides are diagnostics: without MPCQP_DIAGNOSTICS=1 an inherited
+    override (here block caps that change the plan) is ignored and the validated plan is built"""
+    _, _, _, st0 = _lib.analyze(triu_csc(prob20.P), prob20.A)
+    monkeypatch.setenv("MPCQP_CAPM", "96")
+    monkeypatch.setenv("MPCQP_CAPW", "320")
+    monkeypatch.delenv("MPCQP_DIAGNOSTICS", raising=False)
+    _, _, _, st1 = _lib.analyze(triu_csc(prob20.P), prob20.A)
+    assert st1 == st0
+    monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")
+    _, _, _, st2 = _lib.analyze(triu_csc(prob20.P), prob20.A)
+    assert st2 != st0  # the override is honoured with the switch (DESIGN.md: caps 96/320, 16 steps)

@@ -102,3 +102,42 @@ def test_sweep_grid_and_in_track_ics():
     assert np.all(ics[:, 2:] == 0.0)
     X = sweep.scenario_states("radial", 3, 64, 100, 140, ic_seed=3)
     assert np.array_equal(X, rad[np.arange(100, 140) % 64])
+
+
+def _traj_rows(G, lo, hi, steps=7):
+    """a deterministic stand-in for the closed loops' trajectories of global ids [lo, hi) (initial
+    state of each scenario propagated by a fixed linear map, as the device loop records x_true)"""
+    from mpc_arpo_project_amd import sweep
+
+    X = torch.as_tensor(sweep.scenario_states("radial", 5, G // 5, lo, hi, ic_seed=11))
+    M = torch.tensor([[1.0, 0.0, 0.5, 0.0], [0.0, 1.0, 0.0, 0.5], [0.01, 0.0, 0.99, 0.02],
+                      [0.0, -0.01, -0.02, 0.99]], dtype=torch.float64)
+    out = [X]
+    for _ in range(steps):
+        out.append(out[-1] @ M.T)
+    return torch.stack(out, dim=1)  # [hi - lo, steps + 1, 4]
+
+
+def _traj_worker(rank, world, port, G, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mpc_arpo_project_amd import launch, sweep
+
+    lo, hi = launch.shard_range(G, rank, world)
+    full = sweep.gather_traj(_traj_rows(G, lo, hi), G, rank, world, dist)
+    if rank == 0:
+        torch.save(full, out_path)
+    else:
+        assert full is None
+    dist.destroy_process_group()
+
+
+def test_trajectory_gather_matches_single_process(tmp_path):
+    """`sweep --traj`: uneven shards (G = 5 x 11 over 2 and 3 ranks) gathered to rank 0 with
+    sweep.gather_traj equal the single-process trajectories, in global scenario order"""
+    G = 55
+    ref = _traj_rows(G, 0, G)
+    for world in (2, 3):
+        out = str(tmp_path / f"traj{world}.pt")
+        mp.spawn(_traj_worker, args=(world, _free_port(), G, out), nprocs=world, join=True)
+        assert torch.equal(torch.load(out, weights_only=True), ref)

@@ -13,6 +13,7 @@ import torch
 
 import oracle as orc
 from mpc_arpo_project_amd import qp_model, scenarios
+from mpc_arpo_project_amd._lib import MPCQPError
 from mpc_arpo_project_amd.engine import BatchQP
 from mpc_arpo_project_amd.osqp_compat import OSQP
 
@@ -169,6 +170,7 @@ def test_waves_per_instance_do_not_change_results(golden, monkeypatch, Nx, dv, t
     st = dict(eps_abs=1e-4, eps_rel=1e-4)
     outs = []
     for waves, w0diag in (("1", "0"), ("3", "0"), ("3", "1")):
+        monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")  # the overrides are diagnostics
         monkeypatch.setenv("MPCQP_WAVES", waves)
         monkeypatch.setenv("MPCQP_W0DIAG", w0diag)
         qp = BatchQP(prob.P, prob.A, batch=B, **st)
@@ -183,6 +185,95 @@ def test_waves_per_instance_do_not_change_results(golden, monkeypatch, Nx, dv, t
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert np.array_equal(a, b, equal_nan=True)
+
+
+MODES = {  # diagnostic kernel modes (Two waves per instance); "product": no override
+    "product": {}, "w1": dict(MPCQP_WAVES="1"), "w1_matpf": dict(MPCQP_WAVES="1", MPCQP_MATPF="1"),
+    "w2_split": dict(MPCQP_WAVES="2"), "w2_split_matpf": dict(MPCQP_WAVES="2", MPCQP_MATPF="1"),
+    "w3": dict(MPCQP_WAVES="3", MPCQP_W0DIAG="0"), "w3_w0diag": dict(MPCQP_WAVES="3", MPCQP_W0DIAG="1"),
+    "mreg_on": dict(MPCQP_MREG="1", MPCQP_REG_BUDGET="512"), "mreg_off": dict(MPCQP_MREG="0"),
+}
+
+
+def _cold_warm(prob, Ax, l, u, st):
+    qp = BatchQP(prob.P, prob.A, batch=Ax.shape[0], **st)
+    qp.set_data(q=prob.q, Ax=Ax, l=l, u=u)
+    got = []
+    for _ in range(2):  # cold, then warm from the first solve's state
+        r = qp.solve()
+        got += [r.status.cpu().numpy(), r.iter.cpu().numpy(), r.x.cpu().numpy(), r.y.cpu().numpy()]
+    info = qp.schedule_info()
+    qp.close()
+    return got, info
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+@pytest.mark.parametrize("Nx,dv,tag", [(20, False, "batch_n20"), (40, True, "batch_n40dv")])
+def test_later_instances_of_a_wave_equal_the_first(golden, monkeypatch, Nx, dv, tag, mode):
+    """the fixture batch tiled 128 times (B = 8,192: 6 to 16 instances per
+    wave of the persistent grid, so every wave solves several instances in turn -- the pair kernel's
+    instance hand-off, its carried exchange phase and the second-instance-on failure mode of the
+    high-register builds) gives, copy for copy, the bit-identical cold and warm results
+    of the untiled batch (one instance per wave), in every kernel mode"""
+    from conftest import problem
+
+    monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    prob = problem(Nx, dv)
+    d = golden(tag)
+    st = dict(eps_abs=1e-4, eps_rel=1e-4)
+    try:
+        ref, info0 = _cold_warm(prob, d["Ax"], d["l"], d["u"], st)
+    except MPCQPError as e:  # a diagnostic variant above the register budget is refused (below)
+        assert "validated budget" in str(e) and mode != "product", e
+        pytest.skip(f"{mode}: {e}")
+    reps = 8192 // d["Ax"].shape[0]
+    got, info = _cold_warm(prob, np.tile(d["Ax"], (reps, 1)), np.tile(d["l"], (reps, 1)),
+                           np.tile(d["u"], (reps, 1)), st)
+    B0 = d["Ax"].shape[0]
+    per_wave = 8192 / (info["instances_per_cu"] * 256)
+    assert per_wave >= 4, info  # several instances per wave (the grid is one wave-set per CU slot)
+    for a, b in zip(ref, got):
+        for rep in range(reps):
+            assert np.array_equal(a, b[rep * B0:(rep + 1) * B0], equal_nan=True), (mode, rep)
+
+
+@pytest.mark.parametrize("Nx,dv,tag", [(20, False, "batch_n20"), (40, True, "batch_n40dv")])
+def test_matrix_register_kernel_is_bit_identical(golden, monkeypatch, Nx, dv, tag):
+    """KM_MREG (the solve steps' matrix operands held in registers) runs the same plan
+    with the same arithmetic as the LDS-operand kernel: cold and warm solves, tiled so that every
+    wave solves several instances, are bit-identical (where the plan does not qualify -- N = 40,
+    more than 6 steps per solve -- both runs use the LDS kernel)"""
+    from conftest import problem
+
+    monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")
+    monkeypatch.setenv("MPCQP_REG_BUDGET", "512")
+    prob = problem(Nx, dv)
+    d = golden(tag)
+    st = dict(eps_abs=1e-4, eps_rel=1e-4)
+    reps = 4096 // d["Ax"].shape[0]
+    args = (np.tile(d["Ax"], (reps, 1)), np.tile(d["l"], (reps, 1)), np.tile(d["u"], (reps, 1)))
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MPCQP_MREG", flag)
+        outs.append(_cold_warm(prob, *args, st)[0])
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b, equal_nan=True)
+
+
+def test_create_refuses_kernels_above_the_register_budget(monkeypatch, prob20):
+    """mpcqp_create reads the selected kernel's register and scratch
+    allocation (hipFuncGetAttributes) and refuses one above the validated budget; the product
+    kernels sit below it (tests/test_kernel_resources.py checks the code object at build time)"""
+    qp = BatchQP(prob20.P, prob20.A, batch=4)
+    info = qp.schedule_info()
+    assert 0 < info["kernel_regs"] <= 440 and info["kernel_scratch_bytes"] <= 512, info
+    qp.close()
+    monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")
+    monkeypatch.setenv("MPCQP_REG_BUDGET", "128")  # diagnostic: a budget every kernel exceeds
+    with pytest.raises(MPCQPError, match="validated budget"):
+        BatchQP(prob20.P, prob20.A, batch=4)
 
 
 def test_solve_order_does_not_change_results(golden):

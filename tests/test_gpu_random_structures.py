@@ -46,6 +46,7 @@ def test_random_structures_match_oracle(monkeypatch, paired, seed, waves):
     """waves: MPCQP_WAVES -- 0 the automatic choice (one wave for these sizes), 2 two waves with the
     solve steps split between them (their own step packing), 3 two waves with the steps on the first
     (Two waves per instance)"""
+    monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")  # the overrides are diagnostics
     monkeypatch.setenv("MPCQP_PAIRED", paired)
     monkeypatch.setenv("MPCQP_WAVES", waves)
     B = 96

@@ -213,6 +213,15 @@ def test_warm_closed_loop_lockstep():
     for k, fe in enumerate(flips_eng):
         assert fe <= per_step_max[k] + np.sqrt(per_step_max[k]) + 2, (k, flips_eng, flips_floor)
     assert agree[0] >= 0.998, agree
+    # a mean-agreement floor over every warm step: the engine's mean status agreement
+    # with the oracle over steps 1..K-1 is at least the worst floor draw's mean agreement less two
+    # standard deviations of the draws' means -- so a gradual drift spread over many steps, each
+    # inside its per-step bound, still fails
+    n_warm = B * (K - 1)
+    draw_agree = 1.0 - tot / n_warm
+    eng_agree = 1.0 - sum(flips_eng) / n_warm
+    print(f"mean warm-step agreement: engine {eng_agree:.5f}, floor draws {draw_agree.round(5).tolist()}")
+    assert eng_agree >= draw_agree.min() - 2 * draw_agree.std(ddof=1), (eng_agree, draw_agree)
     assert len(fast_diff) <= 1e-3 * n_fast, fast_diff[:8]
 
 

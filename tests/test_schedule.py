@@ -29,6 +29,7 @@ def test_emulated_schedule_solves_kkt(monkeypatch, Nx, dv, waves):
     reference's scripts (Nx 20-50) up to the largest the (4, 8) bucket accepts"""
     from conftest import problem
 
+    monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")  # the overrides are diagnostics
     monkeypatch.setenv("MPCQP_WAVES", waves)
 
     prob = problem(Nx, dv)
@@ -59,6 +60,7 @@ def test_layout_optimiser_lowers_modelled_lds_cycles(monkeypatch):
     P, A = triu_csc(prob.P), sorted_csc(prob.A)
     args = (P, A, 1e-6, np.ones(A.shape[0]), np.ones(P.shape[0] + A.shape[0]))
     _, opt = _lib.schedule_check(*args)
+    monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")  # the overrides are diagnostics
     monkeypatch.setenv("MPCQP_NO_ANNEAL", "1")
     _, greedy = _lib.schedule_check(*args)
     tot = lambda d: d["read"] + d["atomic"] + d["vec"]
@@ -77,6 +79,7 @@ def test_emulated_schedule_random_structures(monkeypatch, paired, seed, copy_row
     solve the KKT system of random sparse QPs, not only the MPC structure the planner was tuned on;
     with the product's copy rows and last-level fold (4), the identity term folded everywhere (2)
     and block-0 copy rows only (0)"""
+    monkeypatch.setenv("MPCQP_DIAGNOSTICS", "1")  # the overrides are diagnostics
     monkeypatch.setenv("MPCQP_PAIRED", paired)
     monkeypatch.setenv("MPCQP_COPY_ROWS", copy_rows)
     monkeypatch.setenv("MPCQP_WAVES", waves)

@@ -2,6 +2,7 @@
 # A/B of engine builds on one box: the default bench (no CPU baseline, no config-3 leg) with each
 # library, alternating.  Extra bench flags in AB_ARGS (e.g. AB_ARGS="--split 1 --steps 10").
 # usage: tools/ab_libs.sh <tag> <rounds> lib1.so lib2.so ...   (paths relative to the repo root)
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-ab}"; mkdir -p "$O"; cd "$R"
 N=${2:-1}; shift 2

@@ -2,6 +2,7 @@
 # A/B of kernel variants by environment: each argument is "tag:ENV=val,ENV=val" (empty env: the
 # default).  Bench at N = 40 delta-v and N = 40 continuous acceleration (--nx 40), 10 steps after 3.
 #   usage: tools/ab_modes.sh <outtag> "w1:MPCQP_WAVES=1" "m2:MPCQP_WAVES=3,MPCQP_W0DIAG=0" ...
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-abm}"; mkdir -p "$O"; cd /tmp && export TMPDIR=/tmp
 shift

@@ -2,6 +2,7 @@
 # Fixed-work ablation libraries (125 ADMM iterations per solve, no checks; each drops one piece of
 # the iteration -- results are meaningless, only the time counts).  Built here, run on the box with
 # tools/ab_libs.sh.   usage: tools/abl_build.sh
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -e
 cd "$(dirname "$0")/.."
 S="mpc_arpo_project_amd/csrc"

@@ -3,6 +3,7 @@
 # extra AGPRs held live (tools/ab/pad*.so, -DMPCQP_PAD_AGPR, nothing else changed): default bench
 # per build, then a rocprofv3 kernel trace of pad0 and pad56 (per-dispatch start / end of the two
 # shards' launches on their two streams).   usage: tools/cliff.sh <tag>
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-cliff}"; mkdir -p "$O"; cd /tmp && export TMPDIR=/tmp
 for p in 0 24 40 56; do

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Threshold of the register cliff: pad builds around 448 allocated registers, one
 # stream and two streams, status counts against the unpadded build.  usage: tools/cliff2.sh <tag>
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-cliff2}"; mkdir -p "$O"; cd /tmp && export TMPDIR=/tmp
 for p in 0 28 32 36 38 40 44 56; do

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Register-pressure builds vs the product (the r03 "cliff"): SGPR spills to memory
 # (_nosv), AGPR pads, VGPR pads; one stream, status counts.   usage: tools/cliff3.sh <tag> libs...
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-cliff3}"; mkdir -p "$O"; cd /tmp && export TMPDIR=/tmp
 shift

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Occupancy scan: the default bench (1 shard) with the LDS allocation padded so that 1..4 instances
 # fit a CU (MPCQP_LDS_PAD, diagnostic only).  usage: tools/occ_scan.sh <tag> [lib.so]
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-occ}"; mkdir -p "$O"; cd "$R"
 [ -n "$2" ] && export MPCQP_LIBRARY=$R/$2

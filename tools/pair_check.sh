@@ -2,6 +2,7 @@
 # Kernel-variant check: parity tests of the two-wave kernel (MPCQP_WAVES=2) and of the matrix-
 # operand prefetch (MPCQP_MATPF=1), then the bench A/B of the four variants at N = 20 and N = 40
 # delta-v.   usage: tools/pair_check.sh <tag> [steps] [variants...]  (variant = "<waves><pf>", e.g. 10 21)
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-pair}"; mkdir -p "$O"; cd /tmp && export TMPDIR=/tmp
 K=${2:-10}; shift 2

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Phase timing (tools/phase_timing.py, timing build) of the one- and two-wave kernels at N = 20
 # and N = 40, and the bench of both with one shard (--split 1).   usage: tools/pair_phase.sh <tag>
+export MPCQP_DIAGNOSTICS=1  # the MPCQP_* overrides below are diagnostics (symbolic.hpp diag_env)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${1:-pphase}"; mkdir -p "$O"; cd /tmp && export TMPDIR=/tmp
 for nx in 20 40; do
