@@ -158,6 +158,13 @@ int mpcqp_get_state(const mpcqp_handle *h, double *xs, double *zs, double *ys, d
  * counterpart). */
 int mpcqp_set_state(mpcqp_handle *h, const double *xs, const double *zs, const double *ys,
                     const double *rho, const int32_t *has_state);
+/* The data scaling the handle carries between solves (caller device buffers, any may be NULL):
+ * E [B*m], the row equilibration of the last solve (OSQP's scaling->E after its update_A), and the
+ * unscaled P values Pu [B*nnzP] and q [B*n] that the next warm solve rescales -- OSQP 0.6's
+ * unscale_data of the last scaled data, ((P_s c^-1) D^-1) D^-1 and (q_s c^-1) D^-1, so a warm
+ * solve's Ruiz passes start from the same rounded data as osqp_update_A's.  White-box parity tests
+ * (bitwise against the oracle's oqp_get_state / oqp_get_data). */
+int mpcqp_get_scaling(const mpcqp_handle *h, double *E, double *Pu, double *qu);
 
 /* Introspection. */
 int mpcqp_dims(const mpcqp_handle *h, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA,

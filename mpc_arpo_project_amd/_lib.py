@@ -20,7 +20,7 @@ LIB_PATH = (_DIAG and os.environ.get("MPCQP_LIBRARY")) or os.path.join(_HERE, "l
 EXPORTED = (
     "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",
     "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
-    "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_set_order", "mpcqp_get_state", "mpcqp_set_state", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
+    "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_set_order", "mpcqp_get_state", "mpcqp_set_state", "mpcqp_get_scaling", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
     "mpcqp_schedule_check",
     "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind", "mpcqp_schedule_kind",
     "mpcqp_kernel_info",
@@ -109,11 +109,14 @@ def lib():
     # points, for the sanitizer check of the host code, tests/test_sanitize.py) exports the marker
     # mpcqp_host_only_build and nothing that touches a GPU; the product library must export all
     host_only = hasattr(L, "mpcqp_host_only_build")
+    # a diagnostic library of an earlier revision (MPCQP_LIBRARY, A/B runs) may predate a
+    # white-box entry point; the product library must export every symbol
+    diag_lib = LIB_PATH != os.path.join(_HERE, "libmpcqp.so")
 
     def _sig(L, name, what, value):
         fn = getattr(L, name, None)
         if fn is None:
-            if host_only:
+            if host_only or (diag_lib and name in ("mpcqp_get_scaling",)):
                 return
             raise MPCQPError(f"{LIB_PATH} does not export {name}")
         setattr(fn, what, value)
@@ -136,6 +139,7 @@ def lib():
     _sig(L, "mpcqp_copy_data", "argtypes", [vp, dp, dp, dp])
     _sig(L, "mpcqp_get_state", "argtypes", [vp, dp, dp, dp, dp, dp])
     _sig(L, "mpcqp_set_state", "argtypes", [vp, dp, dp, dp, dp, dp])
+    _sig(L, "mpcqp_get_scaling", "argtypes", [vp, dp, dp, dp])
     _sig(L, "mpcqp_set_skip", "argtypes", [vp, dp])
     _sig(L, "mpcqp_set_order", "argtypes", [vp, dp])
     _sig(L, "mpcqp_data_buffers", "argtypes", [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)])

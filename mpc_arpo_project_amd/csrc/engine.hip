@@ -32,6 +32,16 @@
 
 using namespace mpcqp;
 
+// OSQP's arithmetic in the data scaling and the checks: no FMA contraction (hipcc contracts
+// a * b + c by default; OSQP 0.6 as the reference's wheel and the oracle evaluate every product and
+// sum with its own rounding), so the Ruiz passes, the carried data drift, the residual mat-vecs,
+// the termination tests, the rho estimate and the certificates round exactly as OSQP's
+// (tests/test_gpu_scaling_parity.py: bitwise).  Explicit fma() remains where the engine's rounding
+// differs from OSQP's anyway -- the factorization, the triangular solves (their own summation
+// orders) and the per-iteration right-hand side and x / z / y updates around them (one rounding
+// fewer per update; unfused they cost 1.1 % of the headline, DESIGN.md Parity).
+#pragma clang fp contract(off)
+
 #define OSQP_INFTY 1e30
 #define RHO_MIN 1e-06
 #define RHO_MAX 1e06
@@ -86,6 +96,11 @@ struct KParams {
   int32_t* has_state;                        // 0 none, 1 scaled iterates, 2 unscaled guess
   double *x_out, *y_out;
   mpcqp_info info;
+  // OSQP 0.6's data drift (osqp_update_A: unscale_data, overwrite A, scale_data): per instance the
+  // unscaled P values and q that the next solve rescales -- (P_s c^-1) D^-1 D^-1 and (q_s c^-1) D^-1
+  // of this solve's scaling, so a warm solve starts its Ruiz passes from the same rounded data as
+  // OSQP does (set_data / update_lin_cost write the plain P / q into every instance)
+  double *Pw, *qw;  // [B][nnzP], [B][n]
   double* scratch;  // [grid][nnzP + nnzA] scaled P and A values of the wave's current instance
   unsigned int* counter;
   unsigned long long* timing;  // diagnostic builds only (MPCQP_TIMING): cycles per phase
@@ -164,6 +179,39 @@ __device__ __forceinline__ double wave_all(double x) {
 }
 __device__ __forceinline__ double wave_max(double x) { return wave_all<false>(x); }
 __device__ __forceinline__ double wave_sum(double x) { return wave_all<true>(x); }
+// OSQP's sequential sums (lin_alg.c vec_mean / vec_prod, the primal certificate's lhs loop,
+// mat_vec's accumulation into one output): s = ((0 + t_0) + t_1) + ... in index order, the
+// rounding a tree reduction does not reproduce.  The caller stages t_k at buf[k] in LDS; every lane
+// runs the same chain over uniform reads (8 in flight), so the result is wave-uniform.
+__device__ __forceinline__ double seq_sum(const double* buf, int cnt) {
+  double s = 0.0;
+  int k = 0;
+  for (; k + 8 <= cnt; k += 8) {  // scalars, not an array (an array here went to scratch)
+    const double t0 = buf[k], t1 = buf[k + 1], t2 = buf[k + 2], t3 = buf[k + 3];
+    const double t4 = buf[k + 4], t5 = buf[k + 5], t6 = buf[k + 6], t7 = buf[k + 7];
+    s = s + t0, s = s + t1, s = s + t2, s = s + t3;
+    s = s + t4, s = s + t5, s = s + t6, s = s + t7;
+  }
+  for (; k < cnt; ++k) s = s + buf[k];
+  return s;
+}
+// The decision x < thr on OSQP's sequential sum x of cnt staged terms, exactly, without the
+// sequential chain in the common case: a tree sum T of the same terms differs from the sequential
+// one by at most (gamma_{cnt-1} + gamma_{ceil log2 cnt}) sum |t| (Higham, Accuracy and Stability of
+// Numerical Algorithms, 4.2), so when T is farther than a generous bound from thr the sequential
+// sum lies on the same side; only a near-tie runs seq_sum.  T, A = the wave's tree sums of t, |t|.
+__device__ __forceinline__ double sum_slack(double A, int cnt) {
+  return (8.0 * cnt) * (0x1p-53 * A) + 0x1p-1060 * cnt;
+}
+__device__ __forceinline__ bool seq_sum_lt(const double* buf, int cnt, double T, double A, double thr) {
+  const double b = sum_slack(A, cnt);
+  if (T + b < thr) return true;
+  if (T - b >= thr) return false;
+  LDS_FENCE();
+  const bool lt = seq_sum(buf, cnt) < thr;
+  LDS_FENCE();
+  return lt;
+}
 __device__ __forceinline__ double limit_scaling(double d) {
   d = d < MIN_SCALING ? 1.0 : d;
   return d > MAX_SCALING ? MAX_SCALING : d;
@@ -655,9 +703,13 @@ __device__ __forceinline__ void ell_load(const EllDev& e, EllTk<R, KMAX>& t, int
 }
 // mv: the resident scaled values -- the LDS image (Plan::MV slots) or the wave's slab
 // (Plan::mv_global, MV-relative); in: the input vector staged in LDS
+// Every output accumulates its terms in OSQP's order (symbolic.cpp: mat_vec / mat_tpose_vec /
+// the symmetric P x), each product rounded before it is added (no contraction, above).  Long
+// outputs: the products of all lanes staged in LDS (stg, wave-private, long_cnt doubles) and summed
+// in term order by seq_sum.
 template <int R, int KMAX>
 __device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>& t, const double* mv,
-                                          const double* in, double (&out)[R], int lane) {
+                                          const double* in, double (&out)[R], int lane, double* stg) {
   constexpr int LPF = ELL_LPF;
   const uint32_t(&lp)[LPF] = t.lp;
   const uint32_t(&li)[LPF] = t.li;
@@ -673,21 +725,21 @@ __device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>&
     }
     out[r] = s;
   }
-  // long outputs: wave-cooperative sums
   for (int L = 0; L < e.nlong; ++L) {
-    double s = 0.0;
     int t0 = lane;
 #pragma unroll
     for (int k = 0; k < LPF; ++k)
       if (k == L) {
-        if (lane < e.long_cnt[L]) s += mv[lp[k]] * in[li[k]];
+        if (lane < e.long_cnt[L]) stg[lane] = mv[lp[k]] * in[li[k]];
         t0 = lane + 64;
       }
     for (int t = t0; t < e.long_cnt[L]; t += 64) {
       const int q = e.long_off[L] + t;
-      s += mv[e.vpos[q]] * in[e.in[q]];
+      stg[t] = mv[e.vpos[q]] * in[e.in[q]];
     }
-    s = wave_sum(s);
+    LDS_FENCE();
+    const double s = seq_sum(stg, e.long_cnt[L]);
+    LDS_FENCE();
     const int o = e.long_out[L];
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -696,10 +748,10 @@ __device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>&
 }
 template <int R, int KMAX>
 __device__ __forceinline__ void ell_mv(const EllDev& e, const double* mv, const double* in,
-                                       double (&out)[R], int lane) {
+                                       double (&out)[R], int lane, double* stg) {
   EllTk<R, KMAX> t;
   ell_load(e, t, lane);
-  ell_apply(e, t, mv, in, out, lane);
+  ell_apply(e, t, mv, in, out, lane, stg);
 }
 // The Ruiz passes' index lists, loaded once per solve into registers (lane-major, 8 bytes = four
 // u16 slots per load; shared by every instance: L1/L2 hits): the passes then read only values.
@@ -720,6 +772,20 @@ __device__ __forceinline__ void load_idx(const EllDev& e, EllIdx<R, KMAX>& ix, i
       ix.w[r][2 * q] = w.x, ix.w[r][2 * q + 1] = w.y;
     }
   }
+}
+// the index words made opaque (asm "+v"): the LDS addresses derived from them are recomputed where
+// they are used instead of being hoisted out of an enclosing loop into registers
+template <int R, int KMAX>
+__device__ __forceinline__ void opaque_idx(EllIdx<R, KMAX>& ix) {
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int k = 0; k < KMAX / 2; ++k) asm volatile("" : "+v"(ix.w[r][k]));
+}
+template <int N>
+__device__ __forceinline__ void opaque_words(uint32_t (&w)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(w[k]));
 }
 // out[r] = max_k |v[slot]| over the ELL terms of slot r, indices from registers (max is
 // order-free, so any traversal equals OSQP's); long outputs read their slots from global memory
@@ -780,6 +846,22 @@ __device__ __forceinline__ void scale_pa_r(double* v, int S_P, int nnzP, int cnt
       const int k = 64 * (j0 + u) + lane;
       if (k < cnt) v[S_P + k] = x[u];
     }
+  }
+}
+// the inverse of the scaled P values for the next solve (unscale_data: mat_mult_scalar(P, c^-1),
+// mat_premult_diag / mat_postmult_diag(P, D^-1)): out[k] = ((v[S_P + k] c^-1) v[ra_k]) v[ca_k],
+// k < nnzP, the D_temp slots holding D^-1 -- the operand layout of scale_pa_r
+template <int JW>
+__device__ __forceinline__ void unscale_p_r(const double* v, int S_P, int nnzP, const uint32_t (&ra)[JW],
+                                            const uint32_t (&ca)[JW], double cinv, int lane,
+                                            double* out) {
+#pragma unroll
+  for (int j = 0; j < 2 * JW; ++j) {
+    if (64 * j >= nnzP) break;  // wave-uniform
+    const int k = 64 * j + lane;
+    const uint32_t a = (j & 1) ? (ra[j / 2] >> 16) : (ra[j / 2] & 0xffffu);
+    const uint32_t b = (j & 1) ? (ca[j / 2] >> 16) : (ca[j / 2] & 0xffffu);
+    if (k < nnzP) out[k] = ((v[S_P + k] * cinv) * v[a]) * v[b];
   }
 }
 // v[base + k] = src[k] for k < cnt, 8 loads per lane in flight
@@ -901,15 +983,15 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   double pr = 0.0, dr = 0.0;
   T_END(T_RS0, t_r0);
   T_BEGIN(t_r1);
-  ell_mv<RM, ELL_KA>(P.eA, mv, xb, R.Ax, lane);  // padding terms are 0 * x
+  ell_mv<RM, ELL_KA>(P.eA, mv, xb, R.Ax, lane, v + P.CACC);  // padding terms are 0 * x
   TSYNC(R.Ax[0]);
   T_END(T_RS1, t_r1);
   T_BEGIN(t_r2);
-  ell_mv<RN, ELL_KP>(P.eP, mv, xb, R.Px, lane);
+  ell_mv<RN, ELL_KP>(P.eP, mv, xb, R.Px, lane, v + P.CACC);
   TSYNC(R.Px[0]);
   T_END(T_RS2, t_r2);
   T_BEGIN(t_r3);
-  ell_mv<RN, ELL_KAT>(P.eAt, mv, yb, R.Aty, lane);
+  ell_mv<RN, ELL_KAT>(P.eAt, mv, yb, R.Aty, lane, v + P.CACC);
   TSYNC(R.Aty[0]);
   T_END(T_RS3, t_r3);
   T_BEGIN(t_r4);
@@ -951,14 +1033,20 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
   }
   nrm = wave_max(nrm);
   if (!(nrm > DIVISION_TOL)) return false;
-  double lhs = 0.0;
+  // lhs = u' max(dy, 0) + l' min(dy, 0) < eps |dy|, decided on OSQP's sequential sum (the terms
+  // staged in C, free during the checks; seq_sum_lt)
+  double* stg = v + P.CACC;
+  double part = 0.0, apart = 0.0;
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
-    if (i < P.m) lhs += S.u[r] * dmaxd(dy[r], 0.0) + S.l[r] * dmind(dy[r], 0.0);
+    if (i < P.m) {
+      const double t = S.u[r] * dmaxd(dy[r], 0.0) + S.l[r] * dmind(dy[r], 0.0);
+      stg[i] = t;
+      part = part + t, apart = apart + fabs(t);
+    }
   }
-  lhs = wave_sum(lhs);
-  if (!(lhs < eps * nrm)) return false;
+  if (!seq_sum_lt(stg, P.m, wave_sum(part), wave_sum(apart), eps * nrm)) return false;
   double* yb = v + P.W + P.n;
   LDS_FENCE();
 #pragma unroll
@@ -966,7 +1054,7 @@ __device__ __forceinline__ bool is_primal_infeasible(const KParams& p, Inst<RN, 
   LDS_FENCE();
   // A' dy by the residual ELL (same term order as the CSC column traversal, loads batched)
   double aty[RN];
-  ell_mv<RN, ELL_KAT>(P.eAt, mv, yb, aty, lane);
+  ell_mv<RN, ELL_KAT>(P.eAt, mv, yb, aty, lane, v + P.CACC);
   double mx = 0.0;
 #pragma unroll
   for (int r = 0; r < RN; ++r)
@@ -981,19 +1069,21 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
                                    const double* mv, int lane, double eps) {
   const DevPlan& P = p.pl;
   const double thr = OSQP_INFTY * MIN_SCALING;
-  double nrm = 0.0, qdx = 0.0;
+  double nrm = 0.0, part = 0.0, apart = 0.0;
+  double* stg = v + P.CACC;  // q' dx (vec_prod) decided on OSQP's order, the products staged in C
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
     if (j < P.n) {
       nrm = dmaxd(nrm, fabs(Dv[r] * dx[r]));
-      qdx += S.q[r] * dx[r];
+      const double t = S.q[r] * dx[r];
+      stg[j] = t;
+      part = part + t, apart = apart + fabs(t);
     }
   }
   nrm = wave_max(nrm);
   if (!(nrm > DIVISION_TOL)) return false;
-  qdx = wave_sum(qdx);
-  if (!(qdx < S.c * eps * nrm)) return false;
+  if (!seq_sum_lt(stg, P.n, wave_sum(part), wave_sum(apart), S.c * eps * nrm)) return false;
   double* xb = v + P.W;
   LDS_FENCE();
 #pragma unroll
@@ -1001,7 +1091,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
   LDS_FENCE();
   // P dx and A dx by the residual ELLs (same term orders as the symmetric / CSR traversals)
   double pdx[RN];
-  ell_mv<RN, ELL_KP>(P.eP, mv, xb, pdx, lane);
+  ell_mv<RN, ELL_KP>(P.eP, mv, xb, pdx, lane, v + P.CACC);
   double mx = 0.0;
 #pragma unroll
   for (int r = 0; r < RN; ++r)
@@ -1009,7 +1099,7 @@ __device__ __forceinline__ bool is_dual_infeasible(const KParams& p, Inst<RN, RM
   mx = wave_max(mx);
   if (!(mx < S.c * eps * nrm)) return false;
   double adx[RM];
-  ell_mv<RM, ELL_KA>(P.eA, mv, xb, adx, lane);
+  ell_mv<RM, ELL_KA>(P.eA, mv, xb, adx, lane, v + P.CACC);
   int bad = 0;
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
@@ -1130,10 +1220,16 @@ __device__ __forceinline__ bool has_solution(int st) {
 // padding entries read the zero slot S_ZERO, so no LDS read is conditional.  Returns D and E;
 // q, l, u (scaled) and c are left in S.
 template <int RN, int RM>
-__device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<RN, RM>& S,
+__device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs, Inst<RN, RM>& S,
                                               double* v, int lane, double (&D)[RN], double (&E)[RM]) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
+  // P and q: the unscaled values OSQP holds after the previous solve's scaling (hs == 1), else the
+  // set-up data
+  double* const Pw = p.Pw + (size_t)inst * P.nnzP;
+  double* const qw = p.qw + (size_t)inst * n;
+  const double* P_in = hs == 1 ? Pw : p.Px;
+  const double* q_in = hs == 1 ? qw : p.q;
   const double* Ax_in = p.Ax + (size_t)inst * P.nnzA;
   const double* l_in = p.l + (size_t)inst * m;
   const double* u_in = p.u + (size_t)inst * m;
@@ -1159,12 +1255,12 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
     }
   }
   if (lane == 0) v[P.S_ZERO] = 0.0;
-  load_vals(v, P.S_P, p.Px, P.nnzP, lane);
+  load_vals(v, P.S_P, P_in, P.nnzP, lane);
   load_vals(v, P.S_A, Ax_in, P.nnzA, lane);
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int j = lane + 64 * r;
-    S.q[r] = j < n ? p.q[j] : 0.0;
+    S.q[r] = j < n ? q_in[j] : 0.0;
     D[r] = 1.0;
   }
 #pragma unroll
@@ -1183,6 +1279,12 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
 #else
   for (int it = 0; it < p.s.scaling; ++it) {
 #endif
+    // (4, 8) bucket: the passes' operand addresses recomputed in every pass (hoisted out of the
+    // pass loop they held ~190 registers: that kernel's register peak, MPCQP_MAX_KERNEL_REGS)
+    if constexpr (RN >= 4) {
+      opaque_idx(iP), opaque_idx(iAt), opaque_idx(iA);
+      opaque_words(ra), opaque_words(ca);
+    }
     // compute_inf_norm_cols_KKT: columns of [P A'; A 0] (P symmetric from its upper triangle).
     // After the first pass P's column norms are the cost normalisation's norms times its factor
     // c (still pending on P's values): max_k |c x_k| = c max_k |x_k| exactly, rounding being
@@ -1222,17 +1324,28 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
     LDS_FENCE();
     // cost normalization: mean of P's column norms, |q|_inf
     ell_absmax_r(P.eP, iP, v, dpc, lane);
-    double csum = 0.0, qmax = 0.0;
+    // vec_mean of the column norms, summed in index order (staged in the D_temp slots: this
+    // pass's factors are consumed) -- unless a tree sum shows it below |q|_inf by more than the
+    // summation orders can differ (sum_slack; the norms are >= 0): then max(mean, |q|_inf) does
+    // not depend on it
+    double qmax = 0.0, csum = 0.0;
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const int j = lane + 64 * r;
       if (j < n) {
-        csum += dpc[r];
+        v[P.S_DT + j] = dpc[r];
+        csum = csum + dpc[r];
         qmax = dmaxd(qmax, fabs(S.q[r]));
       }
     }
-    double c_temp = wave_sum(csum) / n;
     const double inq = limit_scaling(wave_max(qmax));
+    const double T = wave_sum(csum);
+    double c_temp = inq;
+    if (!((T + sum_slack(T, n)) / n < inq)) {
+      LDS_FENCE();
+      c_temp = seq_sum(v + P.S_DT, n) / n;
+      LDS_FENCE();
+    }
     c_temp = limit_scaling(dmaxd(c_temp, inq));
     c_temp = 1. / c_temp;
     cprev = c_temp;  // P *= c_temp: applied by the next rescale pass (or below, after the last)
@@ -1243,6 +1356,21 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, Inst<R
   }
   for (int k = lane; k < P.nnzP; k += 64) v[P.S_P + k] = v[P.S_P + k] * cprev;
   LDS_FENCE();
+  // the next solve's data (scaling.c unscale_data): q <- (q c^-1) D^-1, P <- ((P c^-1) D^-1) D^-1
+  // with D^-1 = 1 / D and c^-1 = 1 / c as scale_data leaves them; D^-1 staged in the D_temp slots
+  // for the row / column operands of scale_pa_r's layout
+  const double cinv = 1. / S.c;
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = lane + 64 * r;
+    const double di = 1. / D[r];
+    if (j < n) {
+      v[P.S_DT + j] = di;
+      qw[j] = (S.q[r] * cinv) * di;
+    }
+  }
+  LDS_FENCE();
+  unscale_p_r(v, P.S_P, P.nnzP, ra, ca, cinv, lane, Pw);
 }
 
 // end of scale_data: constraint classes, scaled bounds, D / E into the per-wave slab, and the
@@ -1268,8 +1396,12 @@ __device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs,
     const double lc = S.l[r] * ec, uc = S.u[r] * ec;
     const uint32_t t = (lc < -thr && uc > thr) ? CT_FREE : ((uc - lc < RHO_TOL) ? CT_EQ : CT_INEQ);
     S.ct |= t << (2 * r);
-    S.l[r] = E[r] * S.l[r];
-    S.u[r] = E[r] * S.u[r];
+    // warm: the bounds as OSQP leaves them, scaled by the previous E (update_bounds), unscaled by
+    // its inverse and rescaled by the new E (update_A's unscale_data / scale_data)
+    const double eci = 1. / ec;
+    const double lb = hs == 1 ? lc * eci : S.l[r], ub = hs == 1 ? uc * eci : S.u[r];
+    S.l[r] = lb * E[r];
+    S.u[r] = ub * E[r];
     S.Einv[r] = 1. / E[r];
     if (i < m) sb.E[i] = E[r];
   }
@@ -1335,7 +1467,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   T_BEGIN(t_sc);
   {
     double D[RN], E[RM];
-    scale_problem<RN, RM>(p, inst, S, v, lane, D, E);
+    scale_problem<RN, RM>(p, inst, hs, S, v, lane, D, E);
     T_BEGIN(t_sf);
     scale_finish<RN, RM>(p, inst, hs, S, sb, v, mv, lane, D, E);
     T_END(T_SCFIN, t_sf);
@@ -1388,7 +1520,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       if (lane + 64 * r < n) xb[lane + 64 * r] = S.x[r];
     LDS_FENCE();
     double az[RM];
-    ell_mv<RM, ELL_KA>(P.eA, mv, xb, az, lane);  // CSR row order
+    ell_mv<RM, ELL_KA>(P.eA, mv, xb, az, lane, v + P.CACC);  // CSR row order
 #pragma unroll
     for (int r = 0; r < RM; ++r) S.z[r] = lane + 64 * r < m ? az[r] : 0.0;
     LDS_FENCE();
@@ -1416,13 +1548,22 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   // the copy-row selections as word masks in VGPRs (W start = value AND mask: the value or +0.0,
   // bitwise the select it replaces).  Held as compare results they were SGPR pairs spilled to VGPR
   // lanes, two readlanes per slot and pass in the loop (927k vs 925k solves/s)
-  uint32_t wmk[RN + RM], bmk[RN + RM];
+  // The (4, 8) bucket re-derives each mask at its use from the lane's bit word (one v_bfe_i32 on an
+  // opaque per-iteration copy, so it is not hoisted back into registers): 24 VGPRs fewer, which
+  // keeps that kernel inside the validated register budget (MPCQP_MAX_KERNEL_REGS)
+  constexpr bool MASK_REGS = RN < 4;
+  constexpr int NMK = MASK_REGS ? RN + RM : 1;
+  uint32_t wmk[NMK], bmk[NMK];
 #pragma unroll
-  for (int r = 0; r < RN + RM; ++r) {
+  for (int r = 0; r < NMK; ++r) {
     wmk[r] = 0u - ((wcp >> r) & 1u);
     bmk[r] = 0u - ((bcp >> r) & 1u);
     asm volatile("" : "+v"(wmk[r]), "+v"(bmk[r]));
   }
+  auto slot_mask = [&](const uint32_t (&arr)[NMK], uint32_t bits, int r) -> uint32_t {
+    if constexpr (MASK_REGS) return arr[r];
+    return (uint32_t)((int32_t)(bits << (31 - r)) >> 31);
+  };
   auto and_d = [](double x, uint32_t mk) {
     return __hiloint2double((int)((uint32_t)__double2hiint(x) & mk), (int)((uint32_t)__double2loint(x) & mk));
   };
@@ -1436,8 +1577,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   if (!p.s.adaptive_rho) ar_int = 0;
   int chk_left = chk, ar_left = ar_int;  // iterations to the next check / rho adaptation
   int status = MPCQP_UNSOLVED, iter = 0, rho_updates = 0;
-  bool can_check = false;
-  double dx[RN], dy[RM];
+  bool can_check = false, finished = false;
   Resid<RN, RM> R;
   Pipe<SolveOps<PAIRED>> sp;
   PipeC spc;
@@ -1449,11 +1589,17 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   for (iter = 1; iter <= p.s.max_iter; ++iter) {
     T_COUNT(T_ITERS);
     T_BEGIN(t_v0);
+    // OSQP's delta_x / delta_y of this iteration: only this iteration's checks read them (the
+    // checks OSQP runs after its loop run inside the last iteration, below), so they are not
+    // carried across the solves of the next iteration
+    double dx[RN], dy[RM];
     if constexpr (MREG)  // lands while the right-hand side is formed
       prefetch_c(rs_fwd, P.nfwd, (uint32_t)lane, spc);
     else
       prefetch(rs_fwd, P.nfwd, (uint32_t)lane, sp);
     double xp[RN], zp[RM], bz[RM];
+    uint32_t wbits = wcp, bbits = bcp;  // opaque per iteration (slot_mask)
+    if constexpr (!MASK_REGS) asm volatile("" : "+v"(wbits), "+v"(bbits));
     // right-hand side [sigma x - q ; z - rho^-1 y] into the permuted solve vector
     // (lanes past the end of x or z store to the junk slot: no lane masks in the loop)
     // The forward solve accumulates into W, which starts at 0 except on the copy rows
@@ -1461,33 +1607,31 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       xp[r] = S.x[r];
-      const double b = sigma * xp[r] - S.q[r];
+      const double b = fma(sigma, xp[r], -S.q[r]);
 #ifndef MPCQP_ABL_NORHS  // fixed-work ablation builds only (Where the time goes)
       v[wsx[r] + coff] = b;
-      v[wsx[r]] = and_d(b, wmk[r]);
+      v[wsx[r]] = and_d(b, slot_mask(wmk, wbits, r));
 #endif
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       zp[r] = S.z[r];
-      bz[r] = zp[r] - rinv_of(S, r) * S.y[r];
+      bz[r] = fma(-rinv_of(S, r), S.y[r], zp[r]);
 #ifndef MPCQP_ABL_NORHS
       v[wsz[r] + coff] = bz[r];
-      v[wsz[r]] = and_d(bz[r], wmk[RN + r]);
+      v[wsz[r]] = and_d(bz[r], slot_mask(wmk, wbits, RN + r));
 #endif
     }
     LDS_FENCE();
     T_END(T_VEC, t_v0);
     T_END(T_V0, t_v0);
     T_BEGIN(t_fw);
-#ifndef MPCQP_ABL_NOSOLVE
     if constexpr (MREG)
       run_body_r<PAIRED>(rs_fwd, P.nfwd, (uint32_t)lane, v, spc, M.m[0]);
     else if constexpr (MATPF)
       run_body_pf<PAIRED>(rs_fwd, P.nfwd, (uint32_t)lane, v, sp);
     else
       run_body(rs_fwd, P.nfwd, (uint32_t)lane, sops, sp);
-#endif
     T_END(T_FWD, t_fw);
     T_BEGIN(t_v1);
     if constexpr (MREG)  // lands during the diagonal pass
@@ -1508,7 +1652,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       for (int r = 0; r < RN + RM; ++r) {  // C at the immediate distance coff: one ds_write2st64
         const double c = wv[r] * dv[r];
         v[P.W + lane + 64 * r + coff] = c;
-        v[P.W + lane + 64 * r] = and_d(c, bmk[r]);
+        v[P.W + lane + 64 * r] = and_d(c, slot_mask(bmk, bbits, r));
       }
     }
 #endif
@@ -1516,14 +1660,12 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     T_END(T_VEC, t_v1);
     T_END(T_V1, t_v1);
     T_BEGIN(t_bw);
-#ifndef MPCQP_ABL_NOSOLVE
     if constexpr (MREG)
       run_body_r<PAIRED>(rs_bwd, P.nbwd, (uint32_t)lane, v, spc, M.m[1]);
     else if constexpr (MATPF)
       run_body_pf<PAIRED>(rs_bwd, P.nbwd, (uint32_t)lane, v, sp);
     else
       run_body(rs_bwd, P.nbwd, (uint32_t)lane, sops, sp);
-#endif
     T_END(T_BWD, t_bw);
     T_BEGIN(t_v2);
     // x, z, y updates (auxil.c update_x / update_z / update_y).  The solution reads are issued
@@ -1545,16 +1687,16 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const double xt = wx[r];
-      S.x[r] = alpha * xt + alpha_c * xp[r];
+      S.x[r] = fma(alpha, xt, alpha_c * xp[r]);
       dx[r] = S.x[r] - xp[r];
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       const double nu = wz[r];
       const double ri = rinv_of(S, r);
-      const double zt = bz[r] + ri * nu;
-      const double zr = alpha * zt + alpha_c * zp[r];
-      S.z[r] = dmind(dmaxd(zr + ri * S.y[r], S.l[r]), S.u[r]);
+      const double zt = fma(ri, nu, bz[r]);
+      const double zr = fma(alpha, zt, alpha_c * zp[r]);
+      S.z[r] = dmind(dmaxd(fma(ri, S.y[r], zr), S.l[r]), S.u[r]);
       dy[r] = rvec_of(S, r) * (zr - S.z[r]);
       S.y[r] = S.y[r] + dy[r];
     }
@@ -1587,7 +1729,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       T_BEGIN(t_tm);
       status = check_termination(p, S, R, dy, dx, sb, v, mv, clane, false TACC_ARG);
       T_END(T_TERM, t_tm);
-      if (status != 0) break;
+      if (status != 0) {
+        finished = true;
+        break;
+      }
       status = MPCQP_UNSOLVED;
     }
     T_BEGIN(t_ad);
@@ -1617,19 +1762,27 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     }
     T_END(T_ADAPT, t_ad);
     T_END(T_CHECK, t_ck);
+    if (iter == p.s.max_iter) {
+      // osqp.c after the ADMM loop: update_info + check_termination unless the last iteration
+      // checked, then the approximate test -- run here, on this iteration's dx, dy
+      T_BEGIN(t_tl);
+      if (!can_check) {
+        compute_residuals(p, S, R, sb, v, mv, clane TACC_ARG);
+        status = check_termination(p, S, R, dy, dx, sb, v, mv, clane, false TACC_ARG);
+        if (status == 0) status = MPCQP_UNSOLVED;
+      }
+      if (status == MPCQP_UNSOLVED) {
+        const int st = check_termination(p, S, R, dy, dx, sb, v, mv, clane, true TACC_ARG);
+        status = st ? st : MPCQP_MAX_ITER_REACHED;
+      }
+      T_END(T_TAIL, t_tl);
+      finished = true;
+      break;
+    }
   }
-  T_BEGIN(t_tl);
-  if (!can_check) {
-    iter = iter - 1;
-    compute_residuals(p, S, R, sb, v, mv, lane TACC_ARG);
-    status = check_termination(p, S, R, dy, dx, sb, v, mv, lane, false TACC_ARG);
-    if (status == 0) status = MPCQP_UNSOLVED;
-  }
+  if (!finished) status = MPCQP_MAX_ITER_REACHED;  // fixed-work diagnostic builds only
   if (iter > p.s.max_iter) iter = p.s.max_iter;
-  if (status == MPCQP_UNSOLVED) {
-    const int st = check_termination(p, S, R, dy, dx, sb, v, mv, lane, true TACC_ARG);
-    status = st ? st : MPCQP_MAX_ITER_REACHED;
-  }
+  T_BEGIN(t_tl);
 
   // ---------------- objective (compute_obj_val) and store_solution
   const bool sol = has_solution(status);
@@ -1757,6 +1910,12 @@ __global__ void __launch_bounds__(64, KM == KM_MVG ? 2 : MPCQP_WAVES_PER_EU) qp_
 constexpr int PAIR_PIPE = MPCQP_PAIR_PIPE;
 #include "engine_pair.inc"
 
+// dst[b][k] = src[k] for every instance b (the drift buffers' start: set_data, update_lin_cost)
+__global__ void bcast_rows_kernel(double* dst, const double* src, int B, int cnt) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < (size_t)B * cnt) dst[t] = src[t % (size_t)cnt];
+}
+
 // ---------------------------------------------------------------------------------------- host
 int fail(int code, const std::string& msg) { return set_error(code, msg); }
 #define HIPCHK(x)                                                                   \
@@ -1870,6 +2029,7 @@ struct mpcqp_handle {
   DevPlan dp{};
   double *Px = nullptr, *q = nullptr, *Ax = nullptr, *l = nullptr, *u = nullptr;
   double *xs = nullptr, *zs = nullptr, *ys = nullptr, *rho = nullptr, *Ecls = nullptr;
+  double *Pw = nullptr, *qw = nullptr;  // OSQP's data drift (KParams::Pw)
   int32_t* has_state = nullptr;
   double* scratch = nullptr;
   unsigned int* counter = nullptr;
@@ -2009,6 +2169,12 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
       return cleanup_fail(MPCQP_E_INVALID, "internal: C region not at the kernel's distance from W");
     if (pl.SJ > 8 * pl.RN)  // the kernel holds 8 RN row / column slots per lane (scale_problem)
       return cleanup_fail(MPCQP_E_UNSUPPORTED, "too many matrix values for the scaling registers");
+    // the sequential sums stage their terms in the accumulator region C (NKP doubles, free during
+    // the checks): a long mat-vec output's products per wave, the certificates' n / m terms
+    for (const Ell* e : {&pl.ellA, &pl.ellAt, &pl.ellP})
+      for (int L = 0; L < e->nlong; ++L)
+        if (e->long_cnt[L] > pl.NKP / pl.waves)
+          return cleanup_fail(MPCQP_E_UNSUPPORTED, "internal: long mat-vec output exceeds its staging");
 
     // occupancy (LDS image and VGPRs) -> persistent grid
     int dev = 0, ncu = 0;
@@ -2057,6 +2223,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->zs, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->ys, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->Ecls, sizeof(double) * Bz * pl.m) == hipSuccess &&
+            hipMalloc(&h->Pw, sizeof(double) * Bz * std::max(1, pl.nnzP)) == hipSuccess &&
+            hipMalloc(&h->qw, sizeof(double) * Bz * pl.n) == hipSuccess &&
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
             hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid * slab_doubles(pl.n, pl.m, pl.mv_slab)) ==
@@ -2072,11 +2240,21 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
 int mpcqp_destroy(mpcqp_handle* h) {
   if (!h) return 0;
   void* bufs[] = {h->d_blob, h->Px, h->q,    h->Ax,        h->l,       h->u,      h->xs,
-                  h->zs,     h->ys, h->Ecls, h->rho, h->has_state, h->scratch, h->counter};
+                  h->zs,     h->ys, h->Ecls, h->rho, h->has_state, h->scratch, h->counter,
+                  h->Pw,     h->qw};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
   return 0;
+}
+
+// every instance's drift buffer row <- src (device), on the handle's stream
+static hipError_t bcast_rows(mpcqp_handle* h, double* dst, const double* src, int cnt) {
+  const size_t tot = (size_t)h->B * cnt;
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(bcast_rows_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream,
+                     dst, src, h->B, cnt);
+  return hipGetLastError();
 }
 
 int mpcqp_set_data(mpcqp_handle* h, const double* Px, const double* q, const double* Ax,
@@ -2090,6 +2268,8 @@ int mpcqp_set_data(mpcqp_handle* h, const double* Px, const double* q, const dou
   HIPCHK(hipMemcpyAsync(h->l, l, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->u, u, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(hipMemsetAsync(h->has_state, 0, sizeof(int32_t) * B, h->stream));
+  HIPCHK(bcast_rows(h, h->Pw, h->Px, pl.nnzP));
+  HIPCHK(bcast_rows(h, h->qw, h->q, pl.n));
   h->has_data = true;
   return 0;
 }
@@ -2115,6 +2295,9 @@ int mpcqp_update_lin_cost(mpcqp_handle* h, const double* q) {
   if (!h || !q) return fail(MPCQP_E_INVALID, "null argument");
   if (!h->has_data) return fail(MPCQP_E_NODATA, "update before set_data");
   HIPCHK(hipMemcpyAsync(h->q, q, sizeof(double) * h->plan.n, hipMemcpyDeviceToDevice, h->stream));
+  // the next solve rescales the new q itself (OSQP would carry (q D) c unscaled: an ulp apart; the
+  // reference never updates q)
+  HIPCHK(bcast_rows(h, h->qw, h->q, h->plan.n));
   return 0;
 }
 
@@ -2142,6 +2325,7 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   p.B = h->B;
   p.Px = h->Px, p.q = h->q, p.Ax = h->Ax, p.l = h->l, p.u = h->u;
   p.xs = h->xs, p.zs = h->zs, p.ys = h->ys, p.rho_state = h->rho, p.Ecls = h->Ecls;
+  p.Pw = h->Pw, p.qw = h->qw;
   p.has_state = h->has_state;
   p.x_out = x, p.y_out = y;
   if (info) p.info = *info;
@@ -2227,6 +2411,16 @@ int mpcqp_set_state(mpcqp_handle* h, const double* xs, const double* zs, const d
   HIPCHK(hipMemcpyAsync(h->rho, rho, sizeof(double) * B, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->has_state, has_state, sizeof(int32_t) * B, hipMemcpyDeviceToDevice,
                         h->stream));
+  return 0;
+}
+
+int mpcqp_get_scaling(const mpcqp_handle* h, double* E, double* Pu, double* qu) {
+  if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  const size_t B = (size_t)h->B;
+  const Plan& pl = h->plan;
+  if (E) HIPCHK(hipMemcpyAsync(E, h->Ecls, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
+  if (Pu) HIPCHK(hipMemcpyAsync(Pu, h->Pw, sizeof(double) * B * pl.nnzP, hipMemcpyDeviceToDevice, h->stream));
+  if (qu) HIPCHK(hipMemcpyAsync(qu, h->qw, sizeof(double) * B * pl.n, hipMemcpyDeviceToDevice, h->stream));
   return 0;
 }
 

@@ -1344,9 +1344,19 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     for (int k = Ap[j]; k < Ap[j + 1]; ++k) t.push_back({pl.S_A + k, Ai[k]});
     return t;
   }, pl.ellAt);
+  // P x from the upper triangle in OSQP's summation order per output o (lin_alg.c: mat_vec over
+  // the columns j >= o, diagonal first, then mat_tpose_vec's skip-diagonal terms of column o, rows
+  // i < o ascending), so the residuals' P x rounds as OSQP's (the Ruiz column norms read the same
+  // lists: max is order-free)
+  std::vector<std::vector<std::pair<int, int>>> posq(n);
+  for (int j = 0; j < n; j++)
+    for (int p = Pp[j]; p < Pp[j + 1]; p++) posq[Pi[p]].push_back({p, j});  // mat_vec: row Pi[p]
+  for (int j = 0; j < n; j++)
+    for (int p = Pp[j]; p < Pp[j + 1]; p++)
+      if (Pi[p] != j) posq[j].push_back({p, Pi[p]});  // mat_tpose_vec(skip_diag): column j
   ok = ok && make_ell(n, ELL_KP, [&](int j) {
     std::vector<std::pair<int, int>> t;
-    for (auto& e : sym[j]) t.push_back({pl.S_P + e.first, e.second});
+    for (auto& e : posq[j]) t.push_back({pl.S_P + e.first, e.second});
     return t;
   }, pl.ellP);
   if (!ok) {

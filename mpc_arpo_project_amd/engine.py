@@ -218,6 +218,18 @@ class BatchQP:
             "mpcqp_get_state"), xs, zs, ys, rho, hs)
         return dict(x=xs, z=zs, y=ys, rho=rho, has_state=hs)
 
+    def get_scaling(self):
+        """The data scaling carried between solves (mpcqp_get_scaling): E of the last solve [B, m]
+        and the unscaled P values [B, nnzP] / q [B, n] the next warm solve rescales (OSQP 0.6's
+        unscale_data), as new device tensors -- the white-box hook of the oracle's state()/data()"""
+        f = dict(dtype=torch.float64, device=self.device)
+        E = torch.empty(self.B, self.m, **f)
+        Pu = torch.empty(self.B, self.nnzP, **f)
+        qu = torch.empty(self.B, self.n, **f)
+        self._on_stream(lambda: check(_lib.lib().mpcqp_get_scaling(
+            self._h, E.data_ptr(), Pu.data_ptr(), qu.data_ptr()), "mpcqp_get_scaling"), E, Pu, qu)
+        return dict(E=E, Pu=Pu, qu=qu)
+
     def set_state(self, x, z, y, rho, has_state):
         """Overwrite the warm-start state (the reverse of get_state; white-box tests)."""
         f = dict(dtype=torch.float64, device=self.device)

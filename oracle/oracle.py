@@ -91,12 +91,16 @@ def lib():
         L.oqp_batch_update_solve.argtypes = [C.c_int, C.POINTER(C.c_void_p), dp, dp, dp, C.c_int,
                                              dp, ip, ip]
         L.oqp_batch_update_solve.restype = C.c_int
+        L.oqp_get_data.argtypes = [vp, dp, dp, dp, dp]
+        L.oqp_get_data.restype = None
         L.oqp_set_state.argtypes = [vp, dp, dp, dp, C.c_double]
         L.oqp_set_state.restype = C.c_int
         L.oqp_batch_set_state.argtypes = [C.c_int, C.POINTER(C.c_void_p), dp, dp, dp, dp]
         L.oqp_batch_set_state.restype = C.c_int
         L.oqp_set_jitter.argtypes = [vp, C.c_ulonglong]
         L.oqp_set_jitter.restype = None
+        L.oqp_set_solve_order.argtypes = [vp, C.c_int]
+        L.oqp_set_solve_order.restype = None
         _lib = L
     return _lib
 
@@ -173,6 +177,11 @@ class OracleOSQP:
         (random direction, deterministic per seed) before each solve of the ADMM loop"""
         lib().oqp_set_jitter(self._w, int(seed))
 
+    def set_solve_order(self, order: int):
+        """parity-floor diagnostics: 1 / 2 = the KKT solves with every entry's products summed apart
+        (backward sums descending / ascending), 0 = QDLDL's order"""
+        lib().oqp_set_solve_order(self._w, int(order))
+
     def update(self, q=None, l=None, u=None, Px=None, Ax=None, Ax_idx=None):
         L = lib()
         if Px is not None:
@@ -230,6 +239,13 @@ class OracleOSQP:
         lib().oqp_get_state(self._w, _dp(xs), _dp(zs), _dp(ys), _dp(D), _dp(E), C.byref(c))
         return dict(x=xs, z=zs, y=ys, D=D, E=E, c=c.value, rho=lib().oqp_rho(self._w),
                     nnzL=lib().oqp_nnz_L(self._w))
+
+    def data(self):
+        """the current scaled data (P values in upper-CSC order, q, l, u) -- white-box test hook"""
+        Px, q = np.empty(len(self._Px)), np.empty(self.n)
+        l, u = np.empty(self.m), np.empty(self.m)
+        lib().oqp_get_data(self._w, _dp(Px), _dp(q), _dp(l), _dp(u))
+        return dict(Px=Px, q=q, l=l, u=u)
 
     def set_state(self, x, z, y, rho=0.0):
         """overwrite the scaled iterates and rho (white-box hook: start from another solver's

@@ -195,6 +195,7 @@ typedef struct {
   int *iwork;
   unsigned char *bwork;
   double *fwork, *bp;
+  int solve_order; /* parity-floor diagnostics (oqp_set_solve_order), 0 = QDLDL's */
 } kkt_sys;
 
 /* Exact minimum-degree ordering on the symmetric pattern given by an adjacency bitmatrix.
@@ -490,6 +491,31 @@ static int kkt_fill_factor(kkt_sys *s, const csc *P, const csc *A, double sigma,
   int pos = qdldl_factor(s->nk, s->Kp, s->Ki, s->Kx, s->Lp, s->Li, s->Lx, s->D, s->Dinv, s->Lnz,
                          s->etree, s->bwork, s->iwork, s->fwork);
   return pos < 0 ? -1 : 0;
+}
+
+/* Parity-floor diagnostics only (oqp_set_solve_order): QDLDL's three solve phases with every
+ * entry's products summed apart and subtracted once -- forward y_t = b_t - (sum_i L_ti y_i) with the
+ * sum in QDLDL's column order, backward x_i = y_i - (sum_t L_ti x_t) in descending (order 1) or
+ * ascending (order 2) row order.  The same solution in exact arithmetic with another valid rounding:
+ * the class of difference a blocked or atomic-accumulation solve makes (the GPU engine's remaining
+ * arithmetic difference from OSQP, DESIGN.md Parity). */
+static void qdldl_solve_sum(int n, const int *Lp, const int *Li, const double *Lx, const double *Dinv,
+                            double *x, double *acc, int order) {
+  for (int i = 0; i < n; i++) acc[i] = 0.0;
+  for (int i = 0; i < n; i++) {
+    double v = x[i] - acc[i];
+    x[i] = v;
+    for (int j = Lp[i]; j < Lp[i + 1]; j++) acc[Li[j]] += Lx[j] * v;
+  }
+  for (int i = 0; i < n; i++) x[i] *= Dinv[i];
+  for (int i = n - 1; i >= 0; i--) {
+    double sum = 0.0;
+    if (order == 1)
+      for (int j = Lp[i + 1] - 1; j >= Lp[i]; j--) sum += Lx[j] * x[Li[j]];
+    else
+      for (int j = Lp[i]; j < Lp[i + 1]; j++) sum += Lx[j] * x[Li[j]];
+    x[i] = x[i] - sum;
+  }
 }
 
 /* solve K [x; nu] = b in place (original ordering) -- qdldl_interface solve (polish flavour) */
@@ -821,7 +847,10 @@ static void update_xz_tilde(oqp_work *w) {
       s->bp[k] = nextafter(s->bp[k], (x >> 63) ? INFINITY : -INFINITY);
     }
   }
-  qdldl_solve(s->nk, s->Lp, s->Li, s->Lx, s->Dinv, s->bp);
+  if (s->solve_order)
+    qdldl_solve_sum(s->nk, s->Lp, s->Li, s->Lx, s->Dinv, s->bp, s->fwork, s->solve_order);
+  else
+    qdldl_solve(s->nk, s->Lp, s->Li, s->Lx, s->Dinv, s->bp);
   for (int i = 0; i < n; i++) w->xz_tilde[i] = s->bp[s->pinv[i]];
   for (int i = 0; i < m; i++) w->xz_tilde[n + i] += w->rho_inv_vec[i] * s->bp[s->pinv[n + i]];
 }
@@ -1207,6 +1236,10 @@ int oqp_solve(oqp_work *w) {
 
 void oqp_get_x(const oqp_work *w, double *x) { memcpy(x, w->sol_x, sizeof(double) * (size_t)w->n); }
 void oqp_get_y(const oqp_work *w, double *y) { memcpy(y, w->sol_y, sizeof(double) * (size_t)w->m); }
+/* parity-floor diagnostics: order 1 / 2 = the ADMM's KKT solves with every entry's products summed
+ * apart (qdldl_solve_sum), 0 = QDLDL's order */
+void oqp_set_solve_order(oqp_work *w, int order) { w->kkt->solve_order = order; }
+
 /* parity-floor diagnostics: seed != 0 turns on the one-ulp right-hand-side jitter of every KKT
  * solve (update_xz_tilde), with a deterministic per-solver stream; 0 turns it off */
 void oqp_set_jitter(oqp_work *w, unsigned long long seed) {
@@ -1229,6 +1262,15 @@ void oqp_get_state(const oqp_work *w, double *x_s, double *z_s, double *y_s, dou
   if (D) memcpy(D, w->D, sizeof(double) * (size_t)w->n);
   if (E) memcpy(E, w->E, sizeof(double) * (size_t)w->m);
   if (c) *c = w->c;
+}
+
+/* the solver's current (scaled) data: P values (upper CSC, nnzP), q [n], l, u [m] -- white-box tests
+ * of the engine's carried scaling (mpcqp_get_scaling) */
+void oqp_get_data(const oqp_work *w, double *Px, double *q, double *l, double *u) {
+  if (Px) memcpy(Px, w->P->x, sizeof(double) * (size_t)csc_nnz(w->P));
+  if (q) memcpy(q, w->q, sizeof(double) * (size_t)w->n);
+  if (l) memcpy(l, w->l, sizeof(double) * (size_t)w->m);
+  if (u) memcpy(u, w->u, sizeof(double) * (size_t)w->m);
 }
 
 /* White-box hook (parity characterisation only): overwrite the scaled warm-start iterates and

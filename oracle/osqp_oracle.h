@@ -70,6 +70,9 @@ int oqp_solve(oqp_work *w);
 /* parity-floor diagnostics: seed != 0 moves every KKT right-hand side entry by one ulp (random
  * direction, deterministic stream per solver) before each solve of the ADMM loop; 0 = off */
 void oqp_set_jitter(oqp_work *w, unsigned long long seed);
+/* parity-floor diagnostics: the ADMM's KKT solves with every entry's products summed apart and
+ * subtracted once (order 1: backward sums in descending, 2: ascending row order; 0: QDLDL's) */
+void oqp_set_solve_order(oqp_work *w, int order);
 
 /* results of the last solve */
 void oqp_get_x(const oqp_work *w, double *x);
@@ -86,6 +89,9 @@ int oqp_nnz_L(const oqp_work *w);
 /* expose the solver's scaled iterates (warm-start state) and scaling, for white-box tests */
 void oqp_get_state(const oqp_work *w, double *x_s, double *z_s, double *y_s, double *D, double *E,
                    double *c);
+
+/* the current scaled data: P values [nnzP], q [n], l, u [m] (any may be NULL; white-box tests) */
+void oqp_get_data(const oqp_work *w, double *Px, double *q, double *l, double *u);
 
 /* overwrite the scaled iterates (x_s [n], z_s, y_s [m]; any may be NULL) and rho (<= 0: keep),
  * re-factoring on a rho change (osqp_update_rho); the batch form takes [B*n] / [B*m] / [B] arrays.

@@ -43,9 +43,10 @@ def engine_run(prob, X0, nsim, suc_cond, noise, eps, noise_seed=123, id_offset=0
 
 
 def oracle_run(prob, X0, nsim, suc_cond, noise, eps, noise_seed=123, id_offset=0, threads=16,
-               jitter=0):
+               jitter=0, solve_order=0):
     """jitter != 0: every solver moves each KKT right-hand side by one ulp before each solve
-    (oracle set_jitter, seeded per chaser) -- the floor of a different summation order"""
+    (oracle set_jitter, seeded per chaser); solve_order != 0: every solver's KKT solves sum each
+    entry's products apart (oracle set_solve_order) -- floors of a different summation order"""
     cl = BatchClosedLoop(prob, X0, noise=noise, noise_seed=noise_seed, id_offset=id_offset,
                          eps_abs=eps, eps_rel=eps)
     cl.enable_tracking(nsim, *suc_cond)
@@ -68,6 +69,8 @@ def oracle_run(prob, X0, nsim, suc_cond, noise, eps, noise_seed=123, id_offset=0
                         warm_start=True, verbose=False)
                 if jitter:
                     s.set_jitter(jitter * 1000003 + b + 1)
+                if solve_order:
+                    s.set_solve_order(solve_order)
                 solvers.append(s)
             x, st, it = orc.batch_update_solve([solvers[b] for b in act], None, None, None, threads)
         else:
@@ -111,7 +114,7 @@ def compare(a, b):
                 same_run=float(np.mean(same_run)))
 
 
-FLOOR_DRAWS = 4
+FLOOR_DRAWS = 6
 
 
 def floor_run(prob, X0, nsim, suc_cond, noise, eps, draw):
@@ -119,11 +122,18 @@ def floor_run(prob, X0, nsim, suc_cond, noise, eps, draw):
     by one ulp (every nonzero coordinate up, resp. down; exact zeros -- the chasers' initial
     velocities -- stay zero: a signed denormal there is a branch input, not a rounding), draws 2
     and 3 keep the initial states and move every KKT right-hand side by one ulp in every solve
-    (two jitter seeds: the backward error of a different summation order, per solve)"""
+    (two jitter seeds: the backward error of a different summation order, per solve), draws 4
+    and 5 run OSQP's KKT solves with every entry's products summed apart before the subtraction
+    (two orders of the backward sums, oracle set_solve_order: an implementation of the same solves
+    with another valid rounding -- the class of the engine's own remaining difference, its
+    blocked / atomic-accumulation triangular solves; everything else it now computes bitwise as
+    OSQP, tests/test_gpu_scaling_parity.py)"""
     if draw < 2:
         X = np.where(X0 == 0, X0, np.nextafter(X0, np.inf if draw == 0 else -np.inf))
         return oracle_run(prob, X, nsim, suc_cond, noise, eps)
-    return oracle_run(prob, X0, nsim, suc_cond, noise, eps, jitter=draw - 1)
+    if draw < 4:
+        return oracle_run(prob, X0, nsim, suc_cond, noise, eps, jitter=draw - 1)
+    return oracle_run(prob, X0, nsim, suc_cond, noise, eps, solve_order=draw - 3)
 
 
 def floor_bound(floors, key, G):

@@ -3,11 +3,12 @@
 i_term, final distance; src/trajectorySimulate.py:359-387, test/disturbRejComp.py:88) compared
 chaser by chaser.  The closed loops are chaotic in the solver's rounding -- the oracle itself,
 restarted from initial states one ulp away, reproduces only ~70 % of its own runs exactly -- so
-the engine is held to that floor: four one-ulp draws of the oracle against itself (two of the
-initial states, two of every solve's right-hand side: sweep_parity.floor_run) give the floor's
-spread, and the engine's agreement with the oracle may not fall below the worst draw by more than
-two of the draws' standard deviations and one scenario (sweep_parity.floor_bound; measured:
-profiles/r04/evidence/parity_printouts.log)."""
+the engine is held to that floor: six draws of the oracle against itself (two of the initial
+states moved by one ulp, two of every solve's right-hand side moved by one ulp, and -- round 5 --
+two of OSQP's KKT solves in another valid summation order, the class of the engine's own remaining
+difference: sweep_parity.floor_run) give the floor's spread, and the engine's agreement with the
+oracle may not fall below the worst draw by more than two of the draws' standard deviations and
+one scenario (sweep_parity.floor_bound; measured: profiles/r05/evidence/sweep_parity_r05.log)."""
 import numpy as np
 import pytest
 
