@@ -171,18 +171,18 @@ def cpu_baseline(prob, X0, steps, warmup, eps, sample, threads, device):
                      "status flip changes its later starting points; see DESIGN.md, Parity")
 
 
-def load_profile(name, B, nx, split, dv=False):
-    """A committed PMC-derived figure (profiles/current/<name>.json or <name>_n<nx>[dv].json,
-    written by tools/pmc_traffic.py or tools/sq_summary.py on the GPU box) for this workload, with
-    the commit it was measured at."""
+def load_profile(name, B, nx, split, dv=False, kind="discrete"):
+    """A committed PMC-derived figure (profiles/current/<name>.json, <name>_n<nx>[dv].json or, for
+    the continuous-time loop, <name>_n<nx>cont.json; written by tools/pmc_traffic.py or
+    tools/sq_summary.py on the GPU box) for this workload, with the commit it was measured at."""
     stem = name[:-len(".json")]
-    for fn in (name, f"{stem}_n{nx}{'dv' if dv else ''}.json"):
+    for fn in (name, f"{stem}_n{nx}{'dv' if dv else ''}.json", f"{stem}_n{nx}cont.json"):
         try:
             pj = json.load(open(os.path.join(REPO, "profiles", "current", fn)))
         except Exception:
             continue
-        if (pj.get("batch") == B and pj.get("nx") == nx and pj.get("concurrent_shards") == split
-                and bool(pj.get("dv", False)) == bool(dv)):
+        if (pj.get("batch") == B and pj.get("nx") == nx and pj.get("concurrent_shards", 1) == split
+                and bool(pj.get("dv", False)) == bool(dv) and pj.get("kind", "discrete") == kind):
             return pj
     return None
 
@@ -316,10 +316,10 @@ def roofline(run, S, K, elapsed):
                     "fraction is claimed from it (the measured HBM figure is `hbm`)"})
 
 
-def attach_profiles(roof, B, nx, S, K, elapsed, dv=False):
+def attach_profiles(roof, B, nx, S, K, elapsed, dv=False, kind="discrete"):
     """HBM traffic (PMC FETCH_SIZE + WRITE_SIZE) and LDS busy share (SQ_LDS_IDX_ACTIVE) from the
     committed profile of this workload, when there is one."""
-    pj = load_profile("pmc_traffic.json", B, nx, S, dv)
+    pj = load_profile("pmc_traffic.json", B, nx, S, dv, kind)
     if pj and pj.get("hbm_bytes_per_launch"):
         t = pj["hbm_bytes_per_launch"]
         ach = t * S * K / elapsed / 1e9
@@ -330,7 +330,7 @@ def attach_profiles(roof, B, nx, S, K, elapsed, dv=False):
                        "measured_at": pj.get("commit"),
                        "what": "PMC FETCH_SIZE + WRITE_SIZE (L2 <-> fabric, calibrated; "
                                "tools/pmc_run.sh)"}
-    sq = load_profile("sq_summary.json", B, nx, S, dv)
+    sq = load_profile("sq_summary.json", B, nx, S, dv, kind)
     if sq and sq.get("lds_array_busy_fraction_if_per_cu") is not None:
         roof["lds_busy"] = {"frac": sq["lds_array_busy_fraction_if_per_cu"],
                             "bank_conflict_share": sq.get("lds_conflict_share"),
@@ -575,6 +575,7 @@ def bench_continuous(args, rank, world, device, dist):
                     cyc_iter=lds_cycles_per_iter(sched["fwd_steps"], sched["bwd_steps"], dims["n"],
                                                  dims["m"], sched["atomics_per_step"]))
     roof["frac_over_solve_launches"] = it_timed * lds_iter / (t_solve.sum() * 1e-3) / 1e9 / LDS_PEAK_GBS
+    attach_profiles(roof, B, nx, 1, K, elapsed, args.dv, kind="continuous")
     return {
         "metric": f"MPC-QP solves/sec @ N={nx} offset-free MPC in the continuous-time nonlinear "
                   f"loop (trajectorySimulateC), batch={B}; ADMM iters to {args.eps:g}",

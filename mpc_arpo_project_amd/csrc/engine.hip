@@ -1577,7 +1577,8 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   if (!p.s.adaptive_rho) ar_int = 0;
   int chk_left = chk, ar_left = ar_int;  // iterations to the next check / rho adaptation
   int status = MPCQP_UNSOLVED, iter = 0, rho_updates = 0;
-  bool can_check = false, finished = false;
+  bool can_check = false;
+  double dx[RN], dy[RM];
   Resid<RN, RM> R;
   Pipe<SolveOps<PAIRED>> sp;
   PipeC spc;
@@ -1589,10 +1590,6 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   for (iter = 1; iter <= p.s.max_iter; ++iter) {
     T_COUNT(T_ITERS);
     T_BEGIN(t_v0);
-    // OSQP's delta_x / delta_y of this iteration: only this iteration's checks read them (the
-    // checks OSQP runs after its loop run inside the last iteration, below), so they are not
-    // carried across the solves of the next iteration
-    double dx[RN], dy[RM];
     if constexpr (MREG)  // lands while the right-hand side is formed
       prefetch_c(rs_fwd, P.nfwd, (uint32_t)lane, spc);
     else
@@ -1729,10 +1726,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       T_BEGIN(t_tm);
       status = check_termination(p, S, R, dy, dx, sb, v, mv, clane, false TACC_ARG);
       T_END(T_TERM, t_tm);
-      if (status != 0) {
-        finished = true;
-        break;
-      }
+      if (status != 0) break;
       status = MPCQP_UNSOLVED;
     }
     T_BEGIN(t_ad);
@@ -1762,27 +1756,19 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     }
     T_END(T_ADAPT, t_ad);
     T_END(T_CHECK, t_ck);
-    if (iter == p.s.max_iter) {
-      // osqp.c after the ADMM loop: update_info + check_termination unless the last iteration
-      // checked, then the approximate test -- run here, on this iteration's dx, dy
-      T_BEGIN(t_tl);
-      if (!can_check) {
-        compute_residuals(p, S, R, sb, v, mv, clane TACC_ARG);
-        status = check_termination(p, S, R, dy, dx, sb, v, mv, clane, false TACC_ARG);
-        if (status == 0) status = MPCQP_UNSOLVED;
-      }
-      if (status == MPCQP_UNSOLVED) {
-        const int st = check_termination(p, S, R, dy, dx, sb, v, mv, clane, true TACC_ARG);
-        status = st ? st : MPCQP_MAX_ITER_REACHED;
-      }
-      T_END(T_TAIL, t_tl);
-      finished = true;
-      break;
-    }
   }
-  if (!finished) status = MPCQP_MAX_ITER_REACHED;  // fixed-work diagnostic builds only
-  if (iter > p.s.max_iter) iter = p.s.max_iter;
   T_BEGIN(t_tl);
+  if (!can_check) {
+    iter = iter - 1;
+    compute_residuals(p, S, R, sb, v, mv, lane TACC_ARG);
+    status = check_termination(p, S, R, dy, dx, sb, v, mv, lane, false TACC_ARG);
+    if (status == 0) status = MPCQP_UNSOLVED;
+  }
+  if (iter > p.s.max_iter) iter = p.s.max_iter;
+  if (status == MPCQP_UNSOLVED) {
+    const int st = check_termination(p, S, R, dy, dx, sb, v, mv, lane, true TACC_ARG);
+    status = st ? st : MPCQP_MAX_ITER_REACHED;
+  }
 
   // ---------------- objective (compute_obj_val) and store_solution
   const bool sol = has_solution(status);

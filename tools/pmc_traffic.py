@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--bench", required=True, help="bench.py JSON line of the PMC runs' workload")
     ap.add_argument("--calib-bytes", type=float, default=float(1 << 30))
     ap.add_argument("--kernel", default=None, help="default: the kernel the bench roofline names")
+    ap.add_argument("--dv", action="store_true", help="the impulsive delta-v model (bench --dv)")
+    ap.add_argument("--kind", default="discrete", help="discrete (closed-loop steps) or continuous "
+                    "(bench.py --continuous: one solve launch per sample period)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
@@ -78,6 +81,8 @@ def main():
         "solves_per_launch": per_launch,
         "concurrent_shards": S,
         "hbm_bytes_per_solve": (read_b + write_b) / per_launch,
+        "kind": a.kind,
+        "dv": bool(a.dv),
     }
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
