@@ -114,7 +114,7 @@ struct KParams {
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
 // s_memtime deltas accumulated per wave in SGPRs, added to p.timing at the end of each instance.
-enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_V0, T_V1, T_V2, T_RS0, T_RS1, T_RS2, T_RS3, T_RS4, T_TM0, T_TM1, T_TM2, T_NSLOT };
+enum { T_SCALE, T_FACTOR, T_FWD, T_BWD, T_VEC, T_CHECK, T_TAIL, T_ITERS, T_NFACT, T_RESID, T_TERM, T_NCHK, T_ADAPT, T_SCFIN, T_V0, T_V1, T_V2, T_RS0, T_RS1, T_RS2, T_RS3, T_RS4, T_TM0, T_TM1, T_TM2, T_SC0, T_SC1, T_SC2, T_SC3, T_SCC, T_NSLOT };
 #ifdef MPCQP_TIMING
 #define T_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define T_END(slot, v) tacc[slot] += __builtin_amdgcn_s_memtime() - (v)
@@ -1221,7 +1221,8 @@ __device__ __forceinline__ bool has_solution(int st) {
 // q, l, u (scaled) and c are left in S.
 template <int RN, int RM>
 __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs, Inst<RN, RM>& S,
-                                              double* v, int lane, double (&D)[RN], double (&E)[RM]) {
+                                              double* v, int lane, double (&D)[RN],
+                                              double (&E)[RM] TACC_PARAM) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
   // P and q: the unscaled values OSQP holds after the previous solve's scaling (hs == 1), else the
@@ -1290,6 +1291,7 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
     // c (still pending on P's values): max_k |c x_k| = c max_k |x_k| exactly, rounding being
     // monotonic (c > 0)
     double dp[RN], da[RN], er[RM], dt[RN], et[RM];
+    T_BEGIN(t_s0);
     if (it == 0) {
       ell_absmax_r(P.eP, iP, v, dp, lane);
     } else {
@@ -1298,6 +1300,9 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
     }
     ell_absmax_r(P.eAt, iAt, v, da, lane);
     ell_absmax_r(P.eA, iA, v, er, lane);
+    TSYNC(er[RM - 1]);
+    T_END(T_SC0, t_s0);
+    T_BEGIN(t_s1);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const int j = lane + 64 * r;
@@ -1313,6 +1318,9 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
       if (i < m) v[P.S_ET + i] = et[r];
     }
     LDS_FENCE();
+    TSYNC(et[RM - 1]);
+    T_END(T_SC1, t_s1);
+    T_BEGIN(t_s2);
     scale_pa_r(v, P.S_P, P.nnzP, P.nnzP + P.nnzA, ra, ca, cprev, lane);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
@@ -1322,6 +1330,9 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
 #pragma unroll
     for (int r = 0; r < RM; ++r) E[r] = E[r] * et[r];
     LDS_FENCE();
+    TSYNC(E[RM - 1]);
+    T_END(T_SC2, t_s2);
+    T_BEGIN(t_s3);
     // cost normalization: mean of P's column norms, |q|_inf
     ell_absmax_r(P.eP, iP, v, dpc, lane);
     // vec_mean of the column norms, summed in index order (staged in the D_temp slots: this
@@ -1345,6 +1356,7 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
       LDS_FENCE();
       c_temp = seq_sum(v + P.S_DT, n) / n;
       LDS_FENCE();
+      T_COUNT(T_SCC);
     }
     c_temp = limit_scaling(dmaxd(c_temp, inq));
     c_temp = 1. / c_temp;
@@ -1353,6 +1365,8 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
     for (int r = 0; r < RN; ++r) S.q[r] = S.q[r] * c_temp;
     S.c = S.c * c_temp;
     LDS_FENCE();
+    TSYNC(S.c);
+    T_END(T_SC3, t_s3);
   }
   for (int k = lane; k < P.nnzP; k += 64) v[P.S_P + k] = v[P.S_P + k] * cprev;
   LDS_FENCE();
@@ -1467,7 +1481,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   T_BEGIN(t_sc);
   {
     double D[RN], E[RM];
-    scale_problem<RN, RM>(p, inst, hs, S, v, lane, D, E);
+    scale_problem<RN, RM>(p, inst, hs, S, v, lane, D, E TACC_ARG);
     T_BEGIN(t_sf);
     scale_finish<RN, RM>(p, inst, hs, S, sb, v, mv, lane, D, E);
     T_END(T_SCFIN, t_sf);

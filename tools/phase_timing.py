@@ -15,7 +15,8 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.environ.get("MPCQP_TIMING_LIB") or os.path.join(REPO, "tools", "libmpcqp_timing.so")
 SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact", "resid", "term", "nchk", "adapt",
-         "scale_finish", "vec_rhs", "vec_diag", "vec_update", "rs_stage", "rs_Ax", "rs_Px", "rs_Aty", "rs_norms", "tm_norms", "tm_pinf", "tm_dinf"]
+         "scale_finish", "vec_rhs", "vec_diag", "vec_update", "rs_stage", "rs_Ax", "rs_Px", "rs_Aty", "rs_norms", "tm_norms", "tm_pinf", "tm_dinf",
+         "sc_norms", "sc_factors", "sc_rescale", "sc_cost", "sc_cost_seq_count"]
 
 
 def build(extra=()):
@@ -23,7 +24,7 @@ def build(extra=()):
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
            "-DMPCQP_TIMING", *extra, os.path.join(csrc, "engine.hip"),
            os.path.join(csrc, "closed_loop.hip"),
-           os.path.join(csrc, "estimation.hip"),
+           os.path.join(csrc, "estimation.hip"), os.path.join(csrc, "host_abi.cpp"),
            os.path.join(csrc, "symbolic.cpp"), os.path.join(csrc, "lds_layout.cpp"),
            os.path.join(csrc, "emulate.cpp"), "-o", LIB]
     subprocess.check_call(cmd)
@@ -75,6 +76,10 @@ def run(B=65536, steps=5, warmup=3, nx=20):
                                 "check_total": t["check"] / max(t["nchk"], 1),
                                 **{k: t[k] / max(t["nchk"], 1) for k in SLOTS if k.startswith(("rs_", "tm_"))}},
            "scale_finish_per_solve": t["scale_finish"] / n_inst,
+           # the Ruiz passes' parts, per pass (scaling passes per solve = settings.scaling, 10)
+           "ruiz_cycles_per_pass": {k: t[k] / (10 * n_inst) for k in ("sc_norms", "sc_factors",
+                                                                   "sc_rescale", "sc_cost")},
+           "ruiz_mean_sequential_share": t["sc_cost_seq_count"] / (10 * n_inst),
            "cycles_per_solve_step": {"fwd": t["fwd"] / iters / sched["fwd_steps"],
                                      "bwd": t["bwd"] / iters / sched["bwd_steps"]},
            "cycles_per_factor_step": t["factor"] / max(t["nfact"], 1) / sched["fac_steps"],
