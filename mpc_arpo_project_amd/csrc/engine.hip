@@ -263,11 +263,14 @@ __device__ __forceinline__ double group_sum(double acc, uint32_t glog, uint32_t 
 
 // Schedule records are read through buffer descriptors: table base and size in SGPRs, the step
 // offset in an SGPR (soffset), the lane's offset a constant VGPR, so no record address is computed
-// per step.  Reads past the table return 0 (buffer range checking).
+// per step.  Every table is followed by TABLE_PAD_STEPS zero steps in device memory (push_table), so
+// the record pipelines load steps up to n + 2 unclamped and in range (round 5: the clamp's n - 1
+// was an SGPR the two-wave kernel spilled, one v_readlane per solve step, +21 % forward-solve time).
+constexpr int TABLE_PAD_STEPS = 3;
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 __device__ __forceinline__ Rsrc table_rsrc(const uint32_t* tbl, int nsteps, int stride_words) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(tbl), (short)0,
-                                           nsteps * stride_words * 4, 0x00020000);
+                                           (nsteps + TABLE_PAD_STEPS) * stride_words * 4, 0x00020000);
 }
 
 // one lane's records of a solve step: 4 segment quads (a0, b0, a1, b1), targets t0..t3 (paired
@@ -385,8 +388,10 @@ struct Pipe {
   typename Ops::Rec a, b, c, d;  // d unused at D = 3
 };
 template <typename Ops>
-__device__ __forceinline__ int step_off(int n, int s) {
-  return (s < n ? s : n - 1) * (Ops::STRIDE * 4);
+__device__ __forceinline__ int step_off(int /*n*/, int s) {  // s <= n + 2: the padded table
+  // readfirstlane: a no-op where the step counter is known uniform; inside the two-wave kernel's
+  // wave-selected branches LLVM otherwise keeps the offset in a VGPR and waterfalls every load
+  return __builtin_amdgcn_readfirstlane(s * (Ops::STRIDE * 4));
 }
 template <typename Ops, int D>
 __device__ __forceinline__ void prefetch(Rsrc rs, int n, uint32_t lane, Pipe<Ops, D>& p) {
@@ -564,8 +569,8 @@ __device__ __forceinline__ void solve_step_r(const SolveRecC& r, const double (&
 struct PipeC {
   SolveRecC a, b, c;
 };
-__device__ __forceinline__ int step_off_c(int n, int s) {
-  return (s < n ? s : n - 1) * (SOLVEC_STEP_WORDS * 4);
+__device__ __forceinline__ int step_off_c(int /*n*/, int s) {  // s <= n + 1: the padded table
+  return __builtin_amdgcn_readfirstlane(s * (SOLVEC_STEP_WORDS * 4));
 }
 __device__ __forceinline__ void prefetch_c(Rsrc rs, int n, uint32_t lane, PipeC& p) {
   __builtin_amdgcn_sched_barrier(0);
@@ -2011,11 +2016,15 @@ void split_records(const Plan& pl, const std::vector<uint32_t>& rec, int nsteps,
 }
 
 template <typename T>
-size_t push_blob(std::vector<char>& blob, const std::vector<T>& v) {
+size_t push_blob(std::vector<char>& blob, const std::vector<T>& v, size_t zero_tail = 0) {
   size_t off = (blob.size() + 15) & ~size_t(15);
-  blob.resize(off + v.size() * sizeof(T) + 16);
+  blob.resize(off + (v.size() + zero_tail) * sizeof(T) + 16);  // resize zero-fills the tail
   if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
   return off;
+}
+// a schedule table and the TABLE_PAD_STEPS zero steps behind it (table_rsrc)
+size_t push_table(std::vector<char>& blob, const std::vector<uint32_t>& v, int stride_words) {
+  return push_blob(blob, v, (size_t)TABLE_PAD_STEPS * stride_words);
 }
 
 }  // namespace
@@ -2090,8 +2099,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     }
     // structure blob
     std::vector<char> blob;
-    size_t o_fac = push_blob(blob, pl.fac), o_tail = push_blob(blob, pl.tail),
-           o_fwd = push_blob(blob, pl.fwd), o_bwd = push_blob(blob, pl.bwd),
+    size_t o_fac = push_table(blob, pl.fac, FAC_STEP_WORDS),
+           o_tail = push_table(blob, pl.tail, FAC_STEP_WORDS),
+           o_fwd = push_table(blob, pl.fwd, SOLVE_STEP_WORDS),
+           o_bwd = push_table(blob, pl.bwd, SOLVE_STEP_WORDS),
            o_Lc = push_blob(blob, pl.Lcol), o_sP = push_blob(blob, pl.slotP),
            o_sA = push_blob(blob, pl.slotA), o_sR = push_blob(blob, pl.slotRho),
            o_sS = push_blob(blob, pl.slotSig), o_wx = push_blob(blob, pl.wsx),
@@ -2116,8 +2127,8 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
       split_records(pl, pl.fwd, pl.nfwd, fwdc, fwdm);
       split_records(pl, pl.bwd, pl.nbwd, bwdc, bwdm);
     }
-    const size_t o_fwdc = push_blob(blob, fwdc), o_fwdm = push_blob(blob, fwdm),
-                 o_bwdc = push_blob(blob, bwdc), o_bwdm = push_blob(blob, bwdm);
+    const size_t o_fwdc = push_table(blob, fwdc, SOLVEC_STEP_WORDS), o_fwdm = push_blob(blob, fwdm),
+                 o_bwdc = push_table(blob, bwdc, SOLVEC_STEP_WORDS), o_bwdm = push_blob(blob, bwdm);
     if (hipMalloc(&h->d_blob, blob.size()) != hipSuccess)
       return cleanup_fail(MPCQP_E_HIP, "hipMalloc(structure)");
     if (hipMemcpy(h->d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
