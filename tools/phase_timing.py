@@ -1,7 +1,7 @@
 """Per-phase cycle breakdown of the QP kernel on the bench workload (diagnostic build).
 
     python tools/phase_timing.py build            # here: hipcc -DMPCQP_TIMING -> tools/libmpcqp_timing.so
-    python tools/phase_timing.py run [B] [steps]  # GPU box: warm closed loop, prints cycles per phase
+    python tools/phase_timing.py run [B] [steps] [warmup] [nx] [dv]  # GPU box: warm closed loop, prints cycles per phase
 
 The timing build stamps s_memtime around scaling, factorization, forward / backward solves, the
 vector work of an ADMM iteration, and the checks (engine.hip, MPCQP_TIMING).  Cycles are s_memtime
@@ -30,7 +30,7 @@ def build(extra=()):
     subprocess.check_call(cmd)
 
 
-def run(B=65536, steps=5, warmup=3, nx=20):
+def run(B=65536, steps=5, warmup=3, nx=20, dv=0):
     os.environ["MPCQP_LIBRARY"] = LIB
     sys.path.insert(0, REPO)
     import ctypes as C
@@ -41,7 +41,7 @@ def run(B=65536, steps=5, warmup=3, nx=20):
 
     L = _lib.lib()
     L.mpcqp_debug_timing.argtypes = [C.c_void_p, C.c_void_p]
-    sim, mpc, fail, deb = scenarios.radial_scenario(Nx=nx)
+    sim, mpc, fail, deb = scenarios.radial_scenario(Nx=nx, isDeltaV=bool(dv))
     prob = qp_model.build_problem(sim, mpc, fail, deb)
     X = scenarios.sample_estimates(B, seed=20250328)[:, :4].copy()
     X[:, 2:4] = 0.0
