@@ -510,10 +510,11 @@ def bench_continuous(args, rank, world, device, dist):
     plant at T_cont = 1 ms with the control held, then the UKF update and the QP rebuild
     (reference test/traj_eval_radialC.py: Nx = 40, noise (0.0012, 0.0012) held 50 samples).
     A step is one sample period; value = QP solves per second over the timed periods, with the
-    per-period split of the solve, plant + UKF + configure time (HIP events)."""
+    per-period split of the solve, plant + UKF + configure time (HIP events; shard 0's stream when
+    the loop runs as --cont-split shards on concurrent HIP streams, ShardedClosedLoopC)."""
     import torch
     from mpc_arpo_project_amd import qp_model, scenarios
-    from mpc_arpo_project_amd.closed_loop import BatchClosedLoopC
+    from mpc_arpo_project_amd.closed_loop import BatchClosedLoopC, ShardedClosedLoopC
     from mpc_arpo_project_amd.mpcsim import Noise
 
     nx = args.nx if args.nx != 20 else 40
@@ -523,27 +524,36 @@ def bench_continuous(args, rank, world, device, dist):
     prob = qp_model.build_problem(sim, mpc, fail, deb)
     B, K, W = args.batch, args.steps, args.warmup
     X0 = initial_states(world * B, rank, B, args.seed)
-    cl = BatchClosedLoopC(prob, X0, T_cont=0.001, T_final=300, mean_motion=sim.mean_mtn,
-                          isDeltaV=args.dv, device=device, noise=noise, id_offset=rank * B,
-                          eps_abs=args.eps, eps_rel=args.eps, longest_first=args.order == "iters")
+    S = max(1, min(args.cont_split, B))
+    kw = dict(T_cont=0.001, T_final=300, mean_motion=sim.mean_mtn, isDeltaV=args.dv, device=device,
+              noise=noise, id_offset=rank * B, eps_abs=args.eps, eps_rel=args.eps,
+              longest_first=args.order == "iters")
+    cl = ShardedClosedLoopC(prob, X0, shards=S, **kw) if S > 1 else BatchClosedLoopC(prob, X0, **kw)
+    parts = cl.parts if S > 1 else [cl]
+    cut = cl.cut if S > 1 else [0, B]
     for _ in range(W):
         cl.period()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
     iters = torch.zeros(K, B, dtype=torch.int32, device=device)
     act = torch.zeros(K, B, dtype=torch.bool, device=device)
-    stream = cl.qp.stream
+    stream = parts[0].qp.stream
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(K):
-        with torch.cuda.stream(stream):
-            act[k].copy_(cl.done == 0, non_blocking=True)
+        for j, c in enumerate(parts):  # each shard's bookkeeping on its own stream
+            with torch.cuda.stream(c.qp.stream):
+                act[k, cut[j]:cut[j + 1]].copy_(c.done == 0, non_blocking=True)
         ev[k][0].record(stream)
-        r = cl.period(on_solved=ev[k][1].record)
-        ev[k][2].record(stream)
-        with torch.cuda.stream(stream):
-            iters[k].copy_(r.iter, non_blocking=True)
+        rs = []
+        for j, c in enumerate(parts):
+            rs.append(c.period(on_solved=ev[k][1].record if j == 0 else None))
+            if j == 0:
+                ev[k][2].record(stream)
+        for j, c in enumerate(parts):
+            with torch.cuda.stream(c.qp.stream):
+                iters[k, cut[j]:cut[j + 1]].copy_(rs[j].iter, non_blocking=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -574,8 +584,10 @@ def bench_continuous(args, rank, world, device, dist):
                     kernel=kernel_name(sched),
                     cyc_iter=lds_cycles_per_iter(sched["fwd_steps"], sched["bwd_steps"], dims["n"],
                                                  dims["m"], sched["atomics_per_step"]))
-    roof["frac_over_solve_launches"] = it_timed * lds_iter / (t_solve.sum() * 1e-3) / 1e9 / LDS_PEAK_GBS
-    attach_profiles(roof, B, nx, 1, K, elapsed, args.dv, kind="continuous")
+    roof["concurrent_shards"] = S
+    if S == 1:  # with shards the solve launches overlap: their own time is not the loop's share
+        roof["frac_over_solve_launches"] = it_timed * lds_iter / (t_solve.sum() * 1e-3) / 1e9 / LDS_PEAK_GBS
+    attach_profiles(roof, B, nx, S, K, elapsed, args.dv, kind="continuous")
     return {
         "metric": f"MPC-QP solves/sec @ N={nx} offset-free MPC in the continuous-time nonlinear "
                   f"loop (trajectorySimulateC), batch={B}; ADMM iters to {args.eps:g}",
@@ -588,10 +600,12 @@ def bench_continuous(args, rank, world, device, dist):
                                f"{dims['n']}, m={dims['m']}, isReject=True) + {nsub} RK45 plant "
                                f"sub-steps at 1 ms (control held) + UKF + configure",
                    "batch_per_gpu": B, "global_batch": world * B, "N": nx,
-                   "parallelism": f"shard{world}" if world > 1 else "single"},
+                   "parallelism": f"shard{world}" if world > 1 else "single",
+                   "streams_per_gpu": S},
         "roofline": roof,
         "period_split_ms": {"solve": float(t_solve.mean()),
-                            "plant_ukf_configure": float(t_rest.mean())},
+                            "plant_ukf_configure": float(t_rest.mean()),
+                            "of": "shard 0" if S > 1 else "the loop"},
         "admm_iters": {"mean": float(it[a].mean()) if a.any() else None,
                        "p90": float(np.percentile(it[a], 90)) if a.any() else None},
         "schedule": sched,
@@ -613,6 +627,8 @@ def main(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle threads (default: every core in this process's affinity mask)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cont-split", type=int, default=2,
+                    help="concurrent HIP-stream shards of the continuous-time loop (config 4)")
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the N=40 legs (config 3 delta-v, N=40 continuous acceleration, "
                          "config 4 continuous-time loop) of the default run")

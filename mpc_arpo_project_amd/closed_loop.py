@@ -483,3 +483,86 @@ class BatchClosedLoopC(BatchClosedLoop):
         if self.noise is not None and self.period_index % int(self.noise[2]) == 0:
             self._draw(self.period_index // int(self.noise[2]))
         return r
+
+
+class ShardedClosedLoopC:
+    """A BatchClosedLoopC split into S shards of consecutive chasers, each on its own HIP stream
+    (ShardedClosedLoop for the continuous-time loop): while one shard's solve launch runs out its
+    tail (config 4's solves run up to max_iter: p90 2,300 ADMM iterations against a mean of ~570),
+    the other shard's solve, plant sub-steps and UKF fill the idle CUs.  Results are identical to
+    the unsharded loop: chasers are independent and keep their global ids (device noise streams,
+    mpcqp_cl_set_ids)."""
+
+    def __init__(self, prob: MPCProblem, x0, T_cont, T_final, mean_motion, shards=2, device="cuda",
+                 id_offset=0, noise_source=None, **kw):
+        x0 = np.asarray(x0, dtype=float)
+        B = x0.shape[0]
+        S = max(1, min(int(shards), B))
+        self.cut = [B * j // S for j in range(S + 1)]
+        dev = torch.device(device)
+        self._draw_k, self._draw_w = None, None
+
+        def shard_source(j):
+            if noise_source is None:
+                return None
+
+            def draw(k, a=self.cut[j], b=self.cut[j + 1]):
+                if self._draw_k != k:
+                    self._draw_w = np.asarray(noise_source(k), dtype=float).reshape(B, 4)
+                    self._draw_k = k
+                return self._draw_w[a:b]
+            return draw
+
+        sts = shard_streams(dev, S) if S > 1 else [None]
+        self.parts = [BatchClosedLoopC(prob, x0[self.cut[j]:self.cut[j + 1]], T_cont, T_final,
+                                       mean_motion, device=dev, id_offset=id_offset + self.cut[j],
+                                       stream=sts[j], noise_source=shard_source(j), **kw)
+                      for j in range(S)]
+        self.B = B
+        self.schedule = self.parts[0].schedule
+        self.nsimC = self.parts[0].nsimC
+        self.qp = self.parts[0].qp  # schedule_info / dims (the same plan in every shard)
+        torch.cuda.synchronize(dev)
+
+    @property
+    def periods(self):
+        return self.parts[0].periods
+
+    @property
+    def period_index(self):
+        return self.parts[0].period_index
+
+    def period(self, on_solved=None):
+        """One sample period of every shard, enqueued shard after shard (async); the solve results
+        of the shards (on_solved(stream) is called after each shard's solve is enqueued)"""
+        return [c.period(on_solved=on_solved) for c in self.parts]
+
+    def _cat(self, name):
+        cur = torch.cuda.current_stream(self.parts[0].device)
+        for c in self.parts:
+            cur.wait_stream(c.qp.stream)
+        return torch.cat([getattr(c, name) for c in self.parts])
+
+    @property
+    def x_true(self):
+        return self._cat("x_true")
+
+    @property
+    def done(self):
+        return self._cat("done")
+
+    @property
+    def iterm(self):
+        return self._cat("iterm")
+
+    @property
+    def ctrl_seq(self):
+        return self._cat("ctrl_seq")
+
+    def synchronize(self):
+        for c in self.parts:
+            c.qp.stream.synchronize()
+
+    def close(self):
+        for c in self.parts:
+            c.close()
