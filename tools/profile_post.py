@@ -50,8 +50,8 @@ def main():
         t, bj = trace_csv(os.path.join(a.src, tdir)), os.path.join(a.src, bench)
         if not t or not os.path.exists(bj):
             continue
-        extra = ["--warmup", "1"] if name == "_continuous" else []
-        out = run([os.path.join(TOOLS, "prof_summary.py"), t, bj] + extra)
+        # the untimed warm-up launches: warmup x concurrent shards (prof_summary's default)
+        out = run([os.path.join(TOOLS, "prof_summary.py"), t, bj])
         open(os.path.join(a.dst, f"prof_summary{name}.json"), "w").write(out)
         shutil.copy(bj, os.path.join(a.dst, f"bench{name}.json"))
         st = glob.glob(os.path.join(a.src, tdir, "**", "*kernel_stats.csv"), recursive=True)

@@ -7,6 +7,8 @@
 #       default workload
 #   tools/profile_r5.sh b <tag>: the same PMC passes for N = 40 delta-v, N = 40 continuous
 #       acceleration and the continuous-time loop; the SQ LDS counters of N = 20 and N = 40 delta-v
+#   tools/profile_r5.sh c <tag>: the calibration, trace and PMC passes of the continuous-time loop
+#       alone (after a change of its layout, e.g. --cont-split)
 # Outputs under gpurun_out/<tag>/; tools/profile_post.py turns them into profiles/current/*.json.
 set -o pipefail
 PART=$1; TAG=${2:-prof_r5}
@@ -19,7 +21,17 @@ pmc() {  # pmc <name> <bench args...>: calibrated FETCH_SIZE + WRITE_SIZE passes
   timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d "$O/write_$n" -o run --output-format csv -- "$@" > "$O/bench_write_$n.json" 2> "$O/bench_write_$n.err" || { echo "write $n failed"; tail -3 "$O/bench_write_$n.err"; exit 1; }
   echo "pmc $n ok"
 }
-if [ "$PART" = a ]; then
+calib() {
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$O/calib_fetch" -o run --output-format csv -- "$R/tools/pmc_calib" > "$O/calib_fetch.log" 2>&1 || { echo calib fetch failed; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/calib_write" -o run --output-format csv -- "$R/tools/pmc_calib" > "$O/calib_write.log" 2>&1 || { echo calib write failed; exit 1; }
+  echo calib ok
+}
+if [ "$PART" = c ]; then
+  calib
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_cont" -o run -- python3 $R/bench.py --continuous --steps 5 --warmup 1 > "$O/bench_cont.json" 2> "$O/trace_cont.err" || { echo cont trace failed; tail -5 "$O/trace_cont.err"; exit 1; }
+  echo "trace_cont: $(head -c 200 $O/bench_cont.json)"
+  pmc cont python3 $R/bench.py --continuous --steps 5 --warmup 1
+elif [ "$PART" = a ]; then
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$O/calib_fetch" -o run --output-format csv -- "$R/tools/pmc_calib" > "$O/calib_fetch.log" 2>&1 || { echo calib fetch failed; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/calib_write" -o run --output-format csv -- "$R/tools/pmc_calib" > "$O/calib_write.log" 2>&1 || { echo calib write failed; exit 1; }
   echo calib ok
