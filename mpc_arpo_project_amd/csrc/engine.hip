@@ -1606,6 +1606,18 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
                            : table_rsrc(P.fwd, P.nfwd, SOLVE_STEP_WORDS);
   const Rsrc rs_bwd = MREG ? table_rsrc(P.bwdc, P.nbwd, SOLVEC_STEP_WORDS)
                            : table_rsrc(P.bwd, P.nbwd, SOLVE_STEP_WORDS);
+  // the diagonal pass's 1/D in registers between factorizations ((2, 4) bucket: 12 VGPRs; six
+  // LDS reads fewer per iteration)
+  constexpr bool DREG = RN == 2 && !MREG;
+  double dvr[DREG ? RN + RM : 1];
+  auto load_dinv = [&](int ln) {
+    if constexpr (DREG) {
+      LDS_FENCE();
+#pragma unroll
+      for (int r = 0; r < RN + RM; ++r) dvr[r] = v[P.DINV + ln + 64 * r];
+    }
+  };
+  load_dinv(lane);
   for (iter = 1; iter <= p.s.max_iter; ++iter) {
     T_COUNT(T_ITERS);
     T_BEGIN(t_v0);
@@ -1662,7 +1674,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
 #pragma unroll
       for (int r = 0; r < RN + RM; ++r) {
         wv[r] = v[P.W + lane + 64 * r];
-        dv[r] = v[P.DINV + lane + 64 * r];
+        if constexpr (DREG)
+          dv[r] = dvr[r];
+        else
+          dv[r] = v[P.DINV + lane + 64 * r];
       }
 #pragma unroll
       for (int r = 0; r < RN + RM; ++r) {  // C at the immediate distance coff: one ds_write2st64
@@ -1764,6 +1779,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
           load_mats(P.fwdm, P.nfwd, (uint32_t)clane, v, M.m[0]);
           load_mats(P.bwdm, P.nbwd, (uint32_t)clane, v, M.m[1]);
         }
+        load_dinv(clane);
 #ifdef MPCQP_TIMING
         const unsigned long long dt_f1 = __builtin_amdgcn_s_memtime() - t_f1;
         tacc[T_FACTOR] += dt_f1;
