@@ -62,7 +62,8 @@ def main():
     for n, suffix, kind, dv, extra in (("n20", "", "discrete", False, []),
                                        ("n40dv", "_n40dv", "discrete", True, ["--dv"]),
                                        ("n40", "_n40", "discrete", False, []),
-                                       ("cont", "_n40cont", "continuous", False, ["--kind", "continuous"])):
+                                       ("cont", "_n40cont", "continuous", False, ["--kind", "continuous"]),
+                                       ("c2", "_n20", "discrete", False, [])):  # config 2 (B = 1,024)
         fe, wr = os.path.join(a.src, f"fetch_{n}"), os.path.join(a.src, f"write_{n}")
         bj = os.path.join(a.src, f"bench_fetch_{n}.json")
         if not (os.path.isdir(fe) and os.path.isdir(wr) and os.path.isdir(cf)):

@@ -7,6 +7,7 @@
 #       default workload
 #   tools/profile_r5.sh b <tag>: the same PMC passes for N = 40 delta-v, N = 40 continuous
 #       acceleration and the continuous-time loop; the SQ LDS counters of N = 20 and N = 40 delta-v
+#   tools/profile_r5.sh d <tag>: calibration + PMC passes of BASELINE config 2 (B = 1,024, N = 20)
 #   tools/profile_r5.sh c <tag>: the calibration, trace and PMC passes of the continuous-time loop
 #       alone (after a change of its layout, e.g. --cont-split)
 # Outputs under gpurun_out/<tag>/; tools/profile_post.py turns them into profiles/current/*.json.
@@ -26,7 +27,10 @@ calib() {
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/calib_write" -o run --output-format csv -- "$R/tools/pmc_calib" > "$O/calib_write.log" 2>&1 || { echo calib write failed; exit 1; }
   echo calib ok
 }
-if [ "$PART" = c ]; then
+if [ "$PART" = d ]; then  # config 2: B = 1,024, N = 20, one stream
+  calib
+  pmc c2 $B --batch 1024 --split 1
+elif [ "$PART" = c ]; then
   calib
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_cont" -o run -- python3 $R/bench.py --continuous --steps 5 --warmup 1 > "$O/bench_cont.json" 2> "$O/trace_cont.err" || { echo cont trace failed; tail -5 "$O/trace_cont.err"; exit 1; }
   echo "trace_cont: $(head -c 200 $O/bench_cont.json)"
