@@ -1618,7 +1618,12 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     }
   };
   load_dinv(lane);
-  for (iter = 1; iter <= p.s.max_iter; ++iter) {
+  // the loop bounds as opaque SGPR values: not rematerialised from the kernel arguments at the
+  // loop head (an s_load whose lgkmcnt(0) wait also drains the LDS queue, every iteration)
+  int max_iter = p.s.max_iter;
+  int chk_s = chk, ar_s = ar_int;
+  asm volatile("" : "+s"(max_iter), "+s"(chk_s), "+s"(ar_s));
+  for (iter = 1; iter <= max_iter; ++iter) {
     T_COUNT(T_ITERS);
     T_BEGIN(t_v0);
     if constexpr (MREG)  // lands while the right-hand side is formed
@@ -1735,10 +1740,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     T_END(T_VEC, t_v2);
     T_END(T_V2, t_v2);
     T_BEGIN(t_ck);
-    can_check = chk && --chk_left == 0;  // iter % chk == 0
-    if (can_check) chk_left = chk;
-    const bool adapt = ar_int && --ar_left == 0;  // iter % ar_int == 0
-    if (adapt) ar_left = ar_int;
+    can_check = chk_s && --chk_left == 0;  // iter % chk == 0
+    if (can_check) chk_left = chk_s;
+    const bool adapt = ar_s && --ar_left == 0;  // iter % ar_int == 0
+    if (adapt) ar_left = ar_s;
     // the check-time code gets an opaque copy of the lane id: its per-lane addresses are
     // recomputed at each check instead of being hoisted out of the ADMM loop into registers (at
     // RN = 4 the hoisted addresses spilled to scratch; MPCQP_OPAQUE_LANE_RN above)
