@@ -198,8 +198,9 @@ def test_device_noise_is_shard_invariant(prob20):
         c.close()
 
 
-def test_sharded_continuous_loop_equals_unsharded():
-    """ShardedClosedLoopC (two shards on two HIP streams, the config-4 bench's layout): every
+@pytest.mark.parametrize("shards", [2, 3])
+def test_sharded_continuous_loop_equals_unsharded(shards):
+    """ShardedClosedLoopC (shards on concurrent HIP streams, the config-4 bench's layout): every
     chaser's plant state, estimate-driven control sequence and termination index equal the
     unsharded loop's bit for bit (device noise keyed by global chaser id, UKF on)."""
     from conftest import problem
@@ -212,7 +213,7 @@ def test_sharded_continuous_loop_equals_unsharded():
     kw = dict(T_cont=0.001, T_final=6, mean_motion=1.107e-3, noise=Noise((0.0012, 0.0012), 50),
               eps_abs=1e-4, eps_rel=1e-4)
     one = BatchClosedLoopC(prob, X, **kw)
-    two = ShardedClosedLoopC(prob, X, shards=2, **kw)
+    two = ShardedClosedLoopC(prob, X, shards=shards, **kw)
     assert two.periods == one.periods
     for _ in range(one.periods):
         ra = one.period()
