@@ -794,13 +794,26 @@ __device__ __forceinline__ void opaque_words(uint32_t (&w)[N]) {
 }
 // out[r] = max_k |v[slot]| over the ELL terms of slot r, indices from registers (max is
 // order-free, so any traversal equals OSQP's); long outputs read their slots from global memory
-template <int R, int KMAX>
-__device__ __forceinline__ void ell_absmax_r(const EllDev& e, const EllIdx<R, KMAX>& ix,
+// kf: bit r = slot r used (ell_kflags, read once per solve: the per-pass kernel-argument reads of
+// e.K[r] were each an s_load with an lgkmcnt(0) wait)
+template <int R>
+__device__ __forceinline__ uint32_t ell_kflags(const EllDev& e) {
+  uint32_t f = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) f |= (e.K[r] != 0 ? 1u : 0u) << r;
+  asm volatile("" : "+v"(f));
+  return f;
+}
+// KF = false ((4, 8) bucket): the flags are not used (there they moved a kernel-argument reload
+// into the ADMM loop head, tests/test_isa_hot_loops.py)
+template <bool KF, int R, int KMAX>
+__device__ __forceinline__ void ell_absmax_r(const EllDev& e, const EllIdx<R, KMAX>& ix, uint32_t kf,
                                              const double* v, double (&out)[R], int lane) {
+  const uint32_t kfu = KF ? __builtin_amdgcn_readfirstlane(kf) : 0u;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     double mx = 0.0;
-    if (e.K[r] != 0) {
+    if (KF ? (kfu & (1u << r)) != 0 : e.K[r] != 0) {
       double b[KMAX];
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
@@ -1246,6 +1259,9 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
   load_idx(P.eP, iP, lane);
   load_idx(P.eAt, iAt, lane);
   load_idx(P.eA, iA, lane);
+  constexpr bool KF = RN == 2;
+  const uint32_t kfP = KF ? ell_kflags<RN>(P.eP) : 0u, kfAt = KF ? ell_kflags<RN>(P.eAt) : 0u,
+                 kfA = KF ? ell_kflags<RM>(P.eA) : 0u;
   constexpr int JW = 4 * RN;  // u16 pairs of row / column slots per lane (Plan::SJ <= 2 JW)
   uint32_t ra[JW], ca[JW];
   {
@@ -1298,13 +1314,13 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
     double dp[RN], da[RN], er[RM], dt[RN], et[RM];
     T_BEGIN(t_s0);
     if (it == 0) {
-      ell_absmax_r(P.eP, iP, v, dp, lane);
+      ell_absmax_r<KF>(P.eP, iP, kfP, v, dp, lane);
     } else {
 #pragma unroll
       for (int r = 0; r < RN; ++r) dp[r] = cprev * dpc[r];
     }
-    ell_absmax_r(P.eAt, iAt, v, da, lane);
-    ell_absmax_r(P.eA, iA, v, er, lane);
+    ell_absmax_r<KF>(P.eAt, iAt, kfAt, v, da, lane);
+    ell_absmax_r<KF>(P.eA, iA, kfA, v, er, lane);
     TSYNC(er[RM - 1]);
     T_END(T_SC0, t_s0);
     T_BEGIN(t_s1);
@@ -1339,7 +1355,7 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
     T_END(T_SC2, t_s2);
     T_BEGIN(t_s3);
     // cost normalization: mean of P's column norms, |q|_inf
-    ell_absmax_r(P.eP, iP, v, dpc, lane);
+    ell_absmax_r<KF>(P.eP, iP, kfP, v, dpc, lane);
     // vec_mean of the column norms, summed in index order (staged in the D_temp slots: this
     // pass's factors are consumed) -- unless a tree sum shows it below |q|_inf by more than the
     // summation orders can differ (sum_slack; the norms are >= 0): then max(mean, |q|_inf) does
