@@ -109,9 +109,14 @@ int mpcqp_destroy(mpcqp_handle *h);
  * l, u [B*m].  Resets the warm-start state of every instance (cold start, rho = settings.rho). */
 int mpcqp_set_data(mpcqp_handle *h, const double *Px, const double *q, const double *Ax,
                    const double *l, const double *u);
-/* New bounds for every instance [B*m] (device). */
+/* New bounds for every instance [B*m] (device).  Alone (no mpcqp_update_A before the next solve)
+ * this is osqp_update_bounds: the instance keeps its data scaling D, E, c -- the next solve re-runs
+ * the Ruiz passes on the same unscaled data as the last scaling did, bitwise the same factors --
+ * and the bounds are scaled by that E once. */
 int mpcqp_update_bounds(mpcqp_handle *h, const double *l, const double *u);
-/* New A values for every instance [B*nnzA] (device, CSC order). */
+/* New A values for every instance [B*nnzA] (device, CSC order): osqp_update_A.  The next solve of
+ * each instance unscales its last scaled data (P, q, and the bounds as mpcqp_update_bounds scaled
+ * them by the previous E), overwrites A and re-runs the Ruiz scaling -- OSQP 0.6's data drift. */
 int mpcqp_update_A(mpcqp_handle *h, const double *Ax);
 /* New shared linear cost q [n] (device). */
 int mpcqp_update_lin_cost(mpcqp_handle *h, const double *q);
@@ -124,8 +129,9 @@ int mpcqp_solve(mpcqp_handle *h, double *x, double *y, const mpcqp_info *info);
 
 /* Zero-copy access to the handle's own problem-data buffers (device): Ax [B*nnzA], l, u [B*m].
  * A producer kernel (e.g. mpcqp_cl_configure) may rewrite them in place between solves, on the
- * handle's stream; the next mpcqp_solve re-scales and re-factors from them (osqp_update_A +
- * osqp_update_bounds semantics). */
+ * handle's stream.  Once Ax has been handed out, every later mpcqp_solve treats each instance as
+ * updated by osqp_update_bounds + osqp_update_A (the reference's per-step pair,
+ * src/trajectorySimulate.py:342,348); l / u alone do not change that. */
 int mpcqp_data_buffers(mpcqp_handle *h, double **Ax, double **l, double **u);
 
 /* Copy the current problem data of every instance into caller device buffers (any may be NULL):
@@ -155,7 +161,8 @@ int mpcqp_get_state(const mpcqp_handle *h, double *xs, double *zs, double *ys, d
                     int32_t *has_state);
 /* The reverse of mpcqp_get_state (device pointers, same layout): overwrite the warm-start state,
  * e.g. with another solver's iterates.  White-box parity tests only (the oracle's oqp_set_state
- * counterpart). */
+ * counterpart).  The data scaling is not part of this state: it stays the handle's own (an
+ * instance this handle never solved scales its set-up data, whatever has_state says). */
 int mpcqp_set_state(mpcqp_handle *h, const double *xs, const double *zs, const double *ys,
                     const double *rho, const int32_t *has_state);
 /* The data scaling the handle carries between solves (caller device buffers, any may be NULL):

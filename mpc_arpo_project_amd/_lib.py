@@ -14,6 +14,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # together with MPCQP_DIAGNOSTICS=1 like every other MPCQP_* override (csrc/symbolic.hpp diag_env);
 # there is no fallback to anything else
 _DIAG = os.environ.get("MPCQP_DIAGNOSTICS") == "1"
+if os.environ.get("MPCQP_LIBRARY") and not _DIAG:
+    # an A/B script that forgot the second variable would otherwise measure the product library
+    raise RuntimeError("MPCQP_LIBRARY is set without MPCQP_DIAGNOSTICS=1: diagnostic libraries "
+                       "load only under MPCQP_DIAGNOSTICS=1")
 LIB_PATH = (_DIAG and os.environ.get("MPCQP_LIBRARY")) or os.path.join(_HERE, "libmpcqp.so")
 
 # every symbol include/mpcqp.h declares (checked by tests/test_abi.py)

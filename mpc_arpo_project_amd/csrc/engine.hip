@@ -100,7 +100,15 @@ struct KParams {
   // unscaled P values and q that the next solve rescales -- (P_s c^-1) D^-1 D^-1 and (q_s c^-1) D^-1
   // of this solve's scaling, so a warm solve starts its Ruiz passes from the same rounded data as
   // OSQP does (set_data / update_lin_cost write the plain P / q into every instance)
-  double *Pw, *qw;  // [B][nnzP], [B][n]
+  // Two buffers each ([2][B][nnzP], [2][B][n]), selected per instance by dsel (drift_of): the input
+  // of the instance's last scaling is kept beside its unscaled output, because a solve after a
+  // bounds-only update (osqp_update_bounds) keeps OSQP's previous scaling -- it re-runs the Ruiz
+  // passes on that same input (bitwise the same D, E, c) -- while a solve after an update of A
+  // (osqp_update_A) rescales the unscaled output.
+  double *Pw, *qw;
+  int32_t* dsel;  // [B] -2 never scaled, -1 last scaled from the shared set-up data, 0 / 1 buffer
+  int32_t* pend;  // [B] A updated since the instance's last solve (mpcqp_update_A)
+  int a_inplace;  // mpcqp_data_buffers handed out the A buffer: every solve follows an update of A
   double* scratch;  // [grid][nnzP + nnzA] scaled P and A values of the wave's current instance
   unsigned int* counter;
   unsigned long long* timing;  // diagnostic builds only (MPCQP_TIMING): cycles per phase
@@ -111,6 +119,36 @@ struct KParams {
   const int32_t* skip;  // [B] or null: instances with skip[i] != 0 are not solved (outputs kept)
   const int32_t* order;  // [B] or null: the k-th instance handed out is order[k] (mpcqp_set_order)
 };
+
+// Where a solve's Ruiz passes start and where the data they leave for the next solve goes (OSQP
+// 0.6's data drift, KParams::Pw).  Wave-uniform.
+struct Drift {
+  const double *P_in, *q_in;  // the unscaled P values / q the Ruiz passes scale
+  double *P_out, *q_out;      // unscale_data of this solve's scaled P / q
+  bool rebound;               // bounds through E_old, E_old^-1, E_new (osqp_update_A after update_bounds)
+  int sel;                    // dsel after this solve
+};
+__device__ __forceinline__ Drift drift_of(const KParams& p, int inst) {
+  const int nP = p.pl.nnzP, n = p.pl.n;
+  const int sel = __builtin_amdgcn_readfirstlane(p.dsel[inst]);
+  const bool dirty = p.a_inplace != 0 || __builtin_amdgcn_readfirstlane(p.pend[inst]) != 0;
+  int in_b, out_b;  // -1: the shared set-up data
+  Drift d;
+  if (sel == -2) {  // first solve after set_data: scale_data of the set-up data (osqp_setup)
+    in_b = -1, out_b = 0, d.rebound = false, d.sel = -1;
+  } else if (dirty) {  // osqp_update_A: unscale_data of the last scaling, then scale_data
+    const int ub = sel == 0 ? 1 : 0;
+    in_b = ub, out_b = 1 - ub, d.rebound = true, d.sel = ub;
+  } else {  // bounds only: the last scaling again (same input, same D, E, c)
+    in_b = sel, out_b = sel == 0 ? 1 : 0, d.rebound = false, d.sel = sel;
+  }
+  const size_t BP = (size_t)p.B * nP, Bq = (size_t)p.B * n;
+  d.P_in = in_b < 0 ? p.Px : p.Pw + in_b * BP + (size_t)inst * nP;
+  d.q_in = in_b < 0 ? p.q : p.qw + in_b * Bq + (size_t)inst * n;
+  d.P_out = p.Pw + out_b * BP + (size_t)inst * nP;
+  d.q_out = p.qw + out_b * Bq + (size_t)inst * n;
+  return d;
+}
 
 // Diagnostic phase timing (-DMPCQP_TIMING builds, tools/phase_timing.py; never the product build):
 // s_memtime deltas accumulated per wave in SGPRs, added to p.timing at the end of each instance.
@@ -1238,17 +1276,16 @@ __device__ __forceinline__ bool has_solution(int st) {
 // padding entries read the zero slot S_ZERO, so no LDS read is conditional.  Returns D and E;
 // q, l, u (scaled) and c are left in S.
 template <int RN, int RM>
-__device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs, Inst<RN, RM>& S,
+__device__ __forceinline__ void scale_problem(const KParams& p, int inst, const Drift& dr, Inst<RN, RM>& S,
                                               double* v, int lane, double (&D)[RN],
                                               double (&E)[RM] TACC_PARAM) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
-  // P and q: the unscaled values OSQP holds after the previous solve's scaling (hs == 1), else the
-  // set-up data
-  double* const Pw = p.Pw + (size_t)inst * P.nnzP;
-  double* const qw = p.qw + (size_t)inst * n;
-  const double* P_in = hs == 1 ? Pw : p.Px;
-  const double* q_in = hs == 1 ? qw : p.q;
+  // P and q: the set-up data, or the unscaled values OSQP holds (drift_of)
+  double* const Pw = dr.P_out;
+  double* const qw = dr.q_out;
+  const double* P_in = dr.P_in;
+  const double* q_in = dr.q_in;
   const double* Ax_in = p.Ax + (size_t)inst * P.nnzA;
   const double* l_in = p.l + (size_t)inst * m;
   const double* u_in = p.u + (size_t)inst * m;
@@ -1412,29 +1449,30 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, int hs
 // scaled values [P | A] copied from the scaling overlay into the resident MV region of the image
 // (read from there by the residual mat-vecs, certificates, KKT (re)assembly and the objective)
 template <int RN, int RM>
-__device__ __forceinline__ void scale_finish(const KParams& p, int inst, int hs, Inst<RN, RM>& S,
+__device__ __forceinline__ void scale_finish(const KParams& p, int inst, bool rebound, Inst<RN, RM>& S,
                                              const Slab& sb, double* v, double* mvw, int lane,
                                              const double (&D)[RN], const double (&E)[RM]) {
   const DevPlan& P = p.pl;
   const int n = P.n, m = P.m;
   S.cinv = 1. / S.c;
-  // constraint classes (auxil.c set_rho_vec / update_rho_vec): with warm state OSQP classifies
-  // on bounds scaled by the PREVIOUS equilibration (update_bounds precedes the rescale of
-  // update_A), on first use by the new one.
+  // constraint classes (auxil.c set_rho_vec / update_rho_vec): after an update of A OSQP
+  // classifies on bounds scaled by the PREVIOUS equilibration (update_bounds precedes the rescale
+  // of update_A); otherwise by the current one (which a bounds-only update keeps).
   const double thr = OSQP_INFTY * MIN_SCALING;
   const double* Eold = p.Ecls + (size_t)inst * m;
   S.ct = 0;
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int i = lane + 64 * r;
-    const double ec = (hs == 1 && i < m) ? Eold[i] : E[r];
+    const double ec = (rebound && i < m) ? Eold[i] : E[r];
     const double lc = S.l[r] * ec, uc = S.u[r] * ec;
     const uint32_t t = (lc < -thr && uc > thr) ? CT_FREE : ((uc - lc < RHO_TOL) ? CT_EQ : CT_INEQ);
     S.ct |= t << (2 * r);
-    // warm: the bounds as OSQP leaves them, scaled by the previous E (update_bounds), unscaled by
-    // its inverse and rescaled by the new E (update_A's unscale_data / scale_data)
+    // after an update of A: the bounds as OSQP leaves them, scaled by the previous E
+    // (update_bounds), unscaled by its inverse and rescaled by the new E (update_A's unscale_data /
+    // scale_data); a bounds-only update scales them by the kept E once
     const double eci = 1. / ec;
-    const double lb = hs == 1 ? lc * eci : S.l[r], ub = hs == 1 ? uc * eci : S.u[r];
+    const double lb = rebound ? lc * eci : S.l[r], ub = rebound ? uc * eci : S.u[r];
     S.l[r] = lb * E[r];
     S.u[r] = ub * E[r];
     S.Einv[r] = 1. / E[r];
@@ -1496,15 +1534,16 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   double* const mv = MVG ? sb.MV : v;
   Inst<RN, RM> S;
   const int hs = p.has_state[inst];
+  const Drift dr = drift_of(p, inst);
 #ifdef MPCQP_TIMING
   unsigned long long tacc[T_NSLOT] = {};
 #endif
   T_BEGIN(t_sc);
   {
     double D[RN], E[RM];
-    scale_problem<RN, RM>(p, inst, hs, S, v, lane, D, E TACC_ARG);
+    scale_problem<RN, RM>(p, inst, dr, S, v, lane, D, E TACC_ARG);
     T_BEGIN(t_sf);
-    scale_finish<RN, RM>(p, inst, hs, S, sb, v, mv, lane, D, E);
+    scale_finish<RN, RM>(p, inst, dr.rebound, S, sb, v, mv, lane, D, E);
     T_END(T_SCFIN, t_sf);
   }
   T_END(T_SCALE, t_sc);
@@ -1879,6 +1918,8 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   if (lane == 0) {
     p.rho_state[inst] = S.rho;
     p.has_state[inst] = 1;
+    p.dsel[inst] = dr.sel;
+    p.pend[inst] = 0;
     if (p.info.status) p.info.status[inst] = status;
     if (p.info.iter) p.info.iter[inst] = iter;
     if (p.info.rho_updates) p.info.rho_updates[inst] = rho_updates;
@@ -1956,6 +1997,17 @@ constexpr int PAIR_PIPE = MPCQP_PAIR_PIPE;
 __global__ void bcast_rows_kernel(double* dst, const double* src, int B, int cnt) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < (size_t)B * cnt) dst[t] = src[t % (size_t)cnt];
+}
+
+// dst[b][k] = the unscaled data the instance's next update of A rescales (drift_of): buffer 1 - dsel
+// (dsel 0), buffer 0 (dsel -1 / 1), the shared set-up data (never scaled)
+__global__ void drift_gather_kernel(double* dst, const double* W, const double* shared,
+                                    const int32_t* dsel, int B, int cnt) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)B * cnt) return;
+  const size_t b = t / (size_t)cnt, k = t % (size_t)cnt;
+  const int sel = dsel[b];
+  dst[t] = sel == -2 ? shared[k] : W[(sel == 0 ? (size_t)B * cnt : 0) + t];
 }
 
 // ---------------------------------------------------------------------------------------- host
@@ -2075,7 +2127,9 @@ struct mpcqp_handle {
   DevPlan dp{};
   double *Px = nullptr, *q = nullptr, *Ax = nullptr, *l = nullptr, *u = nullptr;
   double *xs = nullptr, *zs = nullptr, *ys = nullptr, *rho = nullptr, *Ecls = nullptr;
-  double *Pw = nullptr, *qw = nullptr;  // OSQP's data drift (KParams::Pw)
+  double *Pw = nullptr, *qw = nullptr;  // OSQP's data drift (KParams::Pw): two buffers each
+  int32_t *dsel = nullptr, *pend = nullptr;
+  bool a_inplace = false;  // mpcqp_data_buffers handed out Ax (KParams::a_inplace)
   int32_t* has_state = nullptr;
   double* scratch = nullptr;
   unsigned int* counter = nullptr;
@@ -2271,15 +2325,18 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
             hipMalloc(&h->zs, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->ys, sizeof(double) * Bz * pl.m) == hipSuccess &&
             hipMalloc(&h->Ecls, sizeof(double) * Bz * pl.m) == hipSuccess &&
-            hipMalloc(&h->Pw, sizeof(double) * Bz * std::max(1, pl.nnzP)) == hipSuccess &&
-            hipMalloc(&h->qw, sizeof(double) * Bz * pl.n) == hipSuccess &&
+            hipMalloc(&h->Pw, 2 * sizeof(double) * Bz * std::max(1, pl.nnzP)) == hipSuccess &&
+            hipMalloc(&h->qw, 2 * sizeof(double) * Bz * pl.n) == hipSuccess &&
+            hipMalloc(&h->dsel, sizeof(int32_t) * Bz) == hipSuccess &&
+            hipMalloc(&h->pend, sizeof(int32_t) * Bz) == hipSuccess &&
             hipMalloc(&h->rho, sizeof(double) * Bz) == hipSuccess &&
             hipMalloc(&h->has_state, sizeof(int32_t) * Bz) == hipSuccess &&
             hipMalloc(&h->scratch, sizeof(double) * (size_t)h->grid * slab_doubles(pl.n, pl.m, pl.mv_slab)) ==
                 hipSuccess &&
             hipMalloc(&h->counter, 64) == hipSuccess;
   if (!ok) return cleanup_fail(MPCQP_E_HIP, "hipMalloc(batch buffers)");
-  if (hipMemset(h->has_state, 0, sizeof(int32_t) * Bz) != hipSuccess)
+  if (hipMemset(h->has_state, 0, sizeof(int32_t) * Bz) != hipSuccess ||
+      hipMemsetD32(h->dsel, -2, Bz) != hipSuccess || hipMemset(h->pend, 0, sizeof(int32_t) * Bz) != hipSuccess)
     return cleanup_fail(MPCQP_E_HIP, "hipMemset");
   *out = h;
   return 0;
@@ -2289,7 +2346,7 @@ int mpcqp_destroy(mpcqp_handle* h) {
   if (!h) return 0;
   void* bufs[] = {h->d_blob, h->Px, h->q,    h->Ax,        h->l,       h->u,      h->xs,
                   h->zs,     h->ys, h->Ecls, h->rho, h->has_state, h->scratch, h->counter,
-                  h->Pw,     h->qw};
+                  h->Pw,     h->qw, h->dsel, h->pend};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -2316,8 +2373,9 @@ int mpcqp_set_data(mpcqp_handle* h, const double* Px, const double* q, const dou
   HIPCHK(hipMemcpyAsync(h->l, l, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->u, u, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(hipMemsetAsync(h->has_state, 0, sizeof(int32_t) * B, h->stream));
-  HIPCHK(bcast_rows(h, h->Pw, h->Px, pl.nnzP));
-  HIPCHK(bcast_rows(h, h->qw, h->q, pl.n));
+  // a new setup: the next solve scales the given data (drift_of), no update of A pending
+  HIPCHK(hipMemsetD32Async(h->dsel, -2, B, h->stream));
+  HIPCHK(hipMemsetAsync(h->pend, 0, sizeof(int32_t) * B, h->stream));
   h->has_data = true;
   return 0;
 }
@@ -2336,6 +2394,8 @@ int mpcqp_update_A(mpcqp_handle* h, const double* Ax) {
   if (!h->has_data) return fail(MPCQP_E_NODATA, "update before set_data");
   HIPCHK(hipMemcpyAsync(h->Ax, Ax, sizeof(double) * (size_t)h->B * h->plan.nnzA,
                         hipMemcpyDeviceToDevice, h->stream));
+  // each instance's next solve follows osqp_update_A (unscale, overwrite, rescale: drift_of)
+  HIPCHK(hipMemsetD32Async(h->pend, 1, (size_t)h->B, h->stream));
   return 0;
 }
 
@@ -2344,8 +2404,9 @@ int mpcqp_update_lin_cost(mpcqp_handle* h, const double* q) {
   if (!h->has_data) return fail(MPCQP_E_NODATA, "update before set_data");
   HIPCHK(hipMemcpyAsync(h->q, q, sizeof(double) * h->plan.n, hipMemcpyDeviceToDevice, h->stream));
   // the next solve rescales the new q itself (OSQP would carry (q D) c unscaled: an ulp apart; the
-  // reference never updates q)
+  // reference never updates q): both drift buffers, whichever drift_of picks
   HIPCHK(bcast_rows(h, h->qw, h->q, h->plan.n));
+  HIPCHK(bcast_rows(h, h->qw + (size_t)h->B * h->plan.n, h->q, h->plan.n));
   return 0;
 }
 
@@ -2374,6 +2435,7 @@ int mpcqp_solve(mpcqp_handle* h, double* x, double* y, const mpcqp_info* info) {
   p.Px = h->Px, p.q = h->q, p.Ax = h->Ax, p.l = h->l, p.u = h->u;
   p.xs = h->xs, p.zs = h->zs, p.ys = h->ys, p.rho_state = h->rho, p.Ecls = h->Ecls;
   p.Pw = h->Pw, p.qw = h->qw;
+  p.dsel = h->dsel, p.pend = h->pend, p.a_inplace = h->a_inplace ? 1 : 0;
   p.has_state = h->has_state;
   p.x_out = x, p.y_out = y;
   if (info) p.info = *info;
@@ -2400,6 +2462,8 @@ int mpcqp_debug_timing(mpcqp_handle* h, unsigned long long* dev_buf) {
 
 int mpcqp_data_buffers(mpcqp_handle* h, double** Ax, double** l, double** u) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");
+  // the caller may rewrite A in place between solves: every later solve follows an update of A
+  if (Ax) h->a_inplace = true;
   if (Ax) *Ax = h->Ax;
   if (l) *l = h->l;
   if (u) *u = h->u;
@@ -2467,8 +2531,15 @@ int mpcqp_get_scaling(const mpcqp_handle* h, double* E, double* Pu, double* qu) 
   const size_t B = (size_t)h->B;
   const Plan& pl = h->plan;
   if (E) HIPCHK(hipMemcpyAsync(E, h->Ecls, sizeof(double) * B * pl.m, hipMemcpyDeviceToDevice, h->stream));
-  if (Pu) HIPCHK(hipMemcpyAsync(Pu, h->Pw, sizeof(double) * B * pl.nnzP, hipMemcpyDeviceToDevice, h->stream));
-  if (qu) HIPCHK(hipMemcpyAsync(qu, h->qw, sizeof(double) * B * pl.n, hipMemcpyDeviceToDevice, h->stream));
+  auto gather = [&](double* dst, const double* W, const double* shared, int cnt) {
+    const size_t tot = B * (size_t)cnt;
+    if (tot == 0) return hipSuccess;
+    hipLaunchKernelGGL(drift_gather_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       h->stream, dst, W, shared, h->dsel, (int)B, cnt);
+    return hipGetLastError();
+  };
+  if (Pu) HIPCHK(gather(Pu, h->Pw, h->Px, pl.nnzP));
+  if (qu) HIPCHK(gather(qu, h->qw, h->q, pl.n));
   return 0;
 }
 

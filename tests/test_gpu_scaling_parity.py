@@ -88,3 +88,37 @@ def test_update_lin_cost_restarts_the_q_drift(golden):
     assert np.array_equal(sc["qu"], np.tile(q2, (2, 1)))
     assert not np.array_equal(sc["Pu"][0], triu_csc(P).data)  # the drift of the first solve
     qp.close()
+
+
+@pytest.mark.parametrize("tag,steps,pattern", [("cl_n20", 60, "bounds"), ("cl_n20", 60, "mixed"),
+                                                ("cl_n40dv", 40, "mixed")])
+def test_bounds_only_updates_keep_the_scaling(golden, tag, steps, pattern):
+    """osqp_update_bounds alone keeps OSQP's data scaling (no unscale / rescale round trip): a
+    bounds-only step must leave E, the unscaled P and q bitwise where the oracle leaves them, and
+    an update of A after it must drift from there (before round 6 every warm solve took
+    update_A's path).  'mixed' alternates bounds-only steps with the reference's update pair."""
+    d, P, q, A, l0, u0 = _sequence(golden, tag)
+    Pt = triu_csc(P)
+    st = dict(eps_abs=1e-3, eps_rel=1e-3)
+    o = orc.OracleOSQP()
+    o.setup(P, q, A, l0, u0, warm_start=True, verbose=False, **st)
+    qp = BatchQP(P, A, batch=1, **st)
+    qp.set_data(q=q, Ax=A.data[None, :], l=l0[None, :], u=u0[None, :])
+    for i in range(min(steps, d["step_Ax"].shape[0])):
+        r = qp.solve()
+        ro = o.solve()
+        sc = {k: v.cpu().numpy()[0] for k, v in qp.get_scaling().items()}
+        so, do = o.state(), o.data()
+        Pu, qu = _unscaled(Pt, so, do)
+        assert np.array_equal(sc["E"], so["E"]), (tag, pattern, i)
+        assert np.array_equal(sc["Pu"], Pu), (tag, pattern, i)
+        assert np.array_equal(sc["qu"], qu), (tag, pattern, i)
+        assert int(r.status[0]) == ro.info.status_val, (tag, pattern, i)
+        with_A = pattern == "mixed" and i % 3 == 2
+        o.update(l=d["step_l"][i], u=d["step_u"][i])
+        qp.update(l=d["step_l"][i][None, :], u=d["step_u"][i][None, :])
+        if with_A:
+            o.update(Ax=d["step_Ax"][i], l=d["step_l"][i], u=d["step_u"][i])
+            qp.update(l=d["step_l"][i][None, :], u=d["step_u"][i][None, :],
+                      Ax=d["step_Ax"][i][None, :])
+    qp.close()

@@ -31,6 +31,7 @@ def build(extra=()):
 
 
 def run(B=65536, steps=5, warmup=3, nx=20, dv=0):
+    os.environ["MPCQP_DIAGNOSTICS"] = "1"  # MPCQP_LIBRARY is honoured only with it (_lib.py)
     os.environ["MPCQP_LIBRARY"] = LIB
     sys.path.insert(0, REPO)
     import ctypes as C
