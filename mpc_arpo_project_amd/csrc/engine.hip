@@ -1544,6 +1544,13 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     scale_problem<RN, RM>(p, inst, dr, S, v, lane, D, E TACC_ARG);
     T_BEGIN(t_sf);
     scale_finish<RN, RM>(p, inst, dr.rebound, S, sb, v, mv, lane, D, E);
+    // the drift state after this solve, stored once the scaling has read it (kept to the end of
+    // the solve it was an SGPR live across the ADMM loop; the two-wave kernel's other wave has
+    // read it before the scaling's barriers)
+    if (lane == 0) {
+      p.dsel[inst] = dr.sel;
+      p.pend[inst] = 0;
+    }
     T_END(T_SCFIN, t_sf);
   }
   T_END(T_SCALE, t_sc);
@@ -1918,8 +1925,6 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   if (lane == 0) {
     p.rho_state[inst] = S.rho;
     p.has_state[inst] = 1;
-    p.dsel[inst] = dr.sel;
-    p.pend[inst] = 0;
     if (p.info.status) p.info.status[inst] = status;
     if (p.info.iter) p.info.iter[inst] = iter;
     if (p.info.rho_updates) p.info.rho_updates[inst] = rho_updates;
@@ -2056,11 +2061,17 @@ kernel_fn pick(bool paired, int waves, bool matpf, bool mvg, bool mreg) {
 kernel_fn select_kernel(int n, int m, bool paired, int waves, bool matpf, bool mvg, bool mreg) {
   int rn = 0, rm = 0;
   if (!kernel_bucket(n, m, rn, rm)) return nullptr;
+#ifdef MPCQP_DEV20
+  // diagnostic A/B builds only (tools/dev20.sh): the N = 20 product kernel alone, a 30 s compile
+  if (rn != 2 || waves != 1 || matpf || mvg || mreg) return nullptr;
+  return paired ? qp_batch_kernel<2, 4, true, KM_LDS> : qp_batch_kernel<2, 4, false, KM_LDS>;
+#else
   if (rn == 2) return pick<2, 4>(paired, waves, matpf, mvg, mreg);
 #ifndef MPCQP_ONLY_SMALL
   if (rn == 4) return pick<4, 8>(paired, waves, matpf, mvg, mreg);
 #endif
   return nullptr;
+#endif
 }
 
 // Matrix operands of the solve steps in registers (KM_MREG): one-wave plans of the (2, 4) bucket
@@ -2114,6 +2125,22 @@ size_t push_blob(std::vector<char>& blob, const std::vector<T>& v, size_t zero_t
 // a schedule table and the TABLE_PAD_STEPS zero steps behind it (table_rsrc)
 size_t push_table(std::vector<char>& blob, const std::vector<uint32_t>& v, int stride_words) {
   return push_blob(blob, v, (size_t)TABLE_PAD_STEPS * stride_words);
+}
+// Two tables that run one after the other (forward then backward solve; factorization then its
+// block-inverse tail), laid out as [A][B][the first TABLE_PAD_STEPS steps of A]: the record
+// pipelines' look-ahead loads past the end of A read B's first steps -- the very lines B's own
+// prefetch loads next, then L1 hits -- and B's read A's, which the next iteration loads (the
+// look-ahead loads are never executed, so their content does not matter).  Measured neutral on the
+// N = 20 bench (945k vs 944k solves/s: the shared zero pads were already L1-resident; DESIGN.md,
+// Record traffic), kept because it takes the pads' lines out of the L1 working set.
+void push_chain(std::vector<char>& blob, const std::vector<uint32_t>& A, const std::vector<uint32_t>& B,
+                int stride_words, size_t& oA, size_t& oB) {
+  const size_t pad = (size_t)TABLE_PAD_STEPS * stride_words;
+  std::vector<uint32_t> all(A);
+  all.insert(all.end(), B.begin(), B.end());
+  for (size_t k = 0; k < pad; ++k) all.push_back(k < A.size() ? A[k] : 0u);
+  oA = push_blob(blob, all, pad);
+  oB = oA + A.size() * sizeof(uint32_t);
 }
 
 }  // namespace
@@ -2190,11 +2217,10 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
     }
     // structure blob
     std::vector<char> blob;
-    size_t o_fac = push_table(blob, pl.fac, FAC_STEP_WORDS),
-           o_tail = push_table(blob, pl.tail, FAC_STEP_WORDS),
-           o_fwd = push_table(blob, pl.fwd, SOLVE_STEP_WORDS),
-           o_bwd = push_table(blob, pl.bwd, SOLVE_STEP_WORDS),
-           o_Lc = push_blob(blob, pl.Lcol), o_sP = push_blob(blob, pl.slotP),
+    size_t o_fac = 0, o_tail = 0, o_fwd = 0, o_bwd = 0;
+    push_chain(blob, pl.fac, pl.tail, FAC_STEP_WORDS, o_fac, o_tail);
+    push_chain(blob, pl.fwd, pl.bwd, SOLVE_STEP_WORDS, o_fwd, o_bwd);
+    size_t o_Lc = push_blob(blob, pl.Lcol), o_sP = push_blob(blob, pl.slotP),
            o_sA = push_blob(blob, pl.slotA), o_sR = push_blob(blob, pl.slotRho),
            o_sS = push_blob(blob, pl.slotSig), o_wx = push_blob(blob, pl.wsx),
            o_wz = push_blob(blob, pl.wsz), o_Ap = push_blob(blob, pl.Ap), o_Ai = push_blob(blob, pl.Ai),
