@@ -121,7 +121,33 @@ struct KParams {
 };
 
 // Where a solve's Ruiz passes start and where the data they leave for the next solve goes (OSQP
-// 0.6's data drift, KParams::Pw).  Wave-uniform.
+// 0.6's data drift, KParams::Pw).  Wave-uniform.  drift_sel: the buffer indices; drift_of: the
+// pointers formed from them at the solve's start (one-wave kernel).  The two-wave kernel forms the
+// pointers at their two uses instead: measured per kernel, each form is 1.5-1.9 % faster in its own
+// kernel (register allocation).
+struct DriftSel {
+  int in_b, out_b;  // drift buffer the Ruiz passes scale (-1: the shared set-up data) / unscale into
+  bool rebound;     // bounds through E_old, E_old^-1, E_new (osqp_update_A after update_bounds)
+  int sel;          // dsel after this solve
+};
+__device__ __forceinline__ DriftSel drift_sel(const KParams& p, int inst) {
+  const int sel = __builtin_amdgcn_readfirstlane(p.dsel[inst]);
+  const bool dirty = p.a_inplace != 0 || __builtin_amdgcn_readfirstlane(p.pend[inst]) != 0;
+  DriftSel d;
+  if (sel == -2) {  // first solve after set_data: scale_data of the set-up data (osqp_setup)
+    d.in_b = -1, d.out_b = 0, d.rebound = false, d.sel = -1;
+  } else if (dirty) {  // osqp_update_A: unscale_data of the last scaling, then scale_data
+    const int ub = sel == 0 ? 1 : 0;
+    d.in_b = ub, d.out_b = 1 - ub, d.rebound = true, d.sel = ub;
+  } else {  // bounds only: the last scaling again (same input, same D, E, c)
+    d.in_b = sel, d.out_b = sel == 0 ? 1 : 0, d.rebound = false, d.sel = sel;
+  }
+  return d;
+}
+// the drift buffers' rows of instance inst: P values (cnt = nnzP, base p.Pw) or q (n, p.qw)
+__device__ __forceinline__ double* drift_row(double* base, int b, int B, int cnt, int inst) {
+  return base + ((size_t)b * B + inst) * cnt;
+}
 struct Drift {
   const double *P_in, *q_in;  // the unscaled P values / q the Ruiz passes scale
   double *P_out, *q_out;      // unscale_data of this solve's scaled P / q
@@ -232,6 +258,24 @@ __device__ __forceinline__ double seq_sum(const double* buf, int cnt) {
   }
   for (; k < cnt; ++k) s = s + buf[k];
   return s;
+}
+// two of them at once (independent chains: each add waits for its own chain only), a[0..ca) and
+// b[0..cb): bitwise seq_sum(a, ca) and seq_sum(b, cb)
+__device__ __forceinline__ void seq_sum2(const double* a, int ca, const double* b, int cb, double& sa,
+                                         double& sb) {
+  double x = 0.0, y = 0.0;
+  const int c = ca < cb ? ca : cb;
+  int k = 0;
+  for (; k + 4 <= c; k += 4) {
+    const double a0 = a[k], a1 = a[k + 1], a2 = a[k + 2], a3 = a[k + 3];
+    const double b0 = b[k], b1 = b[k + 1], b2 = b[k + 2], b3 = b[k + 3];
+    x = x + a0, y = y + b0, x = x + a1, y = y + b1;
+    x = x + a2, y = y + b2, x = x + a3, y = y + b3;
+  }
+  for (; k < c; ++k) x = x + a[k], y = y + b[k];
+  for (int j = k; j < ca; ++j) x = x + a[j];
+  for (int j = k; j < cb; ++j) y = y + b[j];
+  sa = x, sb = y;
 }
 // The decision x < thr on OSQP's sequential sum x of cnt staged terms, exactly, without the
 // sequential chain in the common case: a tree sum T of the same terms differs from the sequential
@@ -768,26 +812,42 @@ __device__ __forceinline__ void ell_apply(const EllDev& e, const EllTk<R, KMAX>&
     }
     out[r] = s;
   }
+  if (e.nlong == 0) return;
+  // every long output's products staged first (each output at its own offset: mpcqp_create checks
+  // that they fit), then the sequential sums two at a time
+  int base = 0;
   for (int L = 0; L < e.nlong; ++L) {
     int t0 = lane;
 #pragma unroll
     for (int k = 0; k < LPF; ++k)
       if (k == L) {
-        if (lane < e.long_cnt[L]) stg[lane] = mv[lp[k]] * in[li[k]];
+        if (lane < e.long_cnt[L]) stg[base + lane] = mv[lp[k]] * in[li[k]];
         t0 = lane + 64;
       }
     for (int t = t0; t < e.long_cnt[L]; t += 64) {
       const int q = e.long_off[L] + t;
-      stg[t] = mv[e.vpos[q]] * in[e.in[q]];
+      stg[base + t] = mv[e.vpos[q]] * in[e.in[q]];
     }
-    LDS_FENCE();
-    const double s = seq_sum(stg, e.long_cnt[L]);
-    LDS_FENCE();
-    const int o = e.long_out[L];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (o == lane + 64 * r) out[r] = s;
+    base += e.long_cnt[L];
   }
+  LDS_FENCE();
+  base = 0;
+  for (int L = 0; L < e.nlong; L += 2) {
+    const int c0 = e.long_cnt[L], c1 = L + 1 < e.nlong ? e.long_cnt[L + 1] : 0;
+    double s0, s1 = 0.0;
+    if (c1)
+      seq_sum2(stg + base, c0, stg + base + c0, c1, s0, s1);
+    else
+      s0 = seq_sum(stg + base, c0);
+    const int o0 = e.long_out[L], o1 = c1 ? e.long_out[L + 1] : -1;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (o0 == lane + 64 * r) out[r] = s0;
+      if (o1 == lane + 64 * r) out[r] = s1;
+    }
+    base += c0 + c1;
+  }
+  LDS_FENCE();
 }
 template <int R, int KMAX>
 __device__ __forceinline__ void ell_mv(const EllDev& e, const double* mv, const double* in,
@@ -1039,15 +1099,18 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
   double pr = 0.0, dr = 0.0;
   T_END(T_RS0, t_r0);
   T_BEGIN(t_r1);
-  ell_mv<RM, ELL_KA>(P.eA, mv, xb, R.Ax, lane, v + P.CACC);  // padding terms are 0 * x
-  TSYNC(R.Ax[0]);
-  T_END(T_RS1, t_r1);
-  T_BEGIN(t_r2);
-  ell_mv<RN, ELL_KP>(P.eP, mv, xb, R.Px, lane, v + P.CACC);
-  TSYNC(R.Px[0]);
-  T_END(T_RS2, t_r2);
-  T_BEGIN(t_r3);
-  ell_mv<RN, ELL_KAT>(P.eAt, mv, yb, R.Aty, lane, v + P.CACC);
+  {  // the three mat-vecs' index loads issued together: one L2 round trip instead of three
+     // (+0.8 %)
+    EllTk<RM, ELL_KA> tA;
+    EllTk<RN, ELL_KP> tP;
+    EllTk<RN, ELL_KAT> tT;
+    ell_load(P.eA, tA, lane);
+    ell_load(P.eP, tP, lane);
+    ell_load(P.eAt, tT, lane);
+    ell_apply(P.eA, tA, mv, xb, R.Ax, lane, v + P.CACC);  // padding terms are 0 * x
+    ell_apply(P.eP, tP, mv, xb, R.Px, lane, v + P.CACC);
+    ell_apply(P.eAt, tT, mv, yb, R.Aty, lane, v + P.CACC);
+  }
   TSYNC(R.Aty[0]);
   T_END(T_RS3, t_r3);
   T_BEGIN(t_r4);
@@ -2063,6 +2126,11 @@ kernel_fn select_kernel(int n, int m, bool paired, int waves, bool matpf, bool m
   if (!kernel_bucket(n, m, rn, rm)) return nullptr;
 #ifdef MPCQP_DEV20
   // diagnostic A/B builds only (tools/dev20.sh): the N = 20 product kernel alone, a 30 s compile
+  // (-DMPCQP_DEV40: the N = 40 two-wave product kernel beside it)
+#ifdef MPCQP_DEV40
+  if (rn == 4 && waves == 3 && !matpf && !mvg && !mreg)
+    return paired ? qp_pair_kernel<2, 4, true, 2> : qp_pair_kernel<2, 4, false, 2>;
+#endif
   if (rn != 2 || waves != 1 || matpf || mvg || mreg) return nullptr;
   return paired ? qp_batch_kernel<2, 4, true, KM_LDS> : qp_batch_kernel<2, 4, false, KM_LDS>;
 #else
@@ -2299,10 +2367,12 @@ int mpcqp_create(const mpcqp_structure* st, const mpcqp_settings* s, int32_t bat
       return cleanup_fail(MPCQP_E_UNSUPPORTED, "too many matrix values for the scaling registers");
     // the sequential sums stage their terms in the accumulator region C (NKP doubles, free during
     // the checks): a long mat-vec output's products per wave, the certificates' n / m terms
-    for (const Ell* e : {&pl.ellA, &pl.ellAt, &pl.ellP})
-      for (int L = 0; L < e->nlong; ++L)
-        if (e->long_cnt[L] > pl.NKP / pl.waves)
-          return cleanup_fail(MPCQP_E_UNSUPPORTED, "internal: long mat-vec output exceeds its staging");
+    for (const Ell* e : {&pl.ellA, &pl.ellAt, &pl.ellP}) {
+      int tot = 0;  // a mat-vec stages all its long outputs at once (ell_apply)
+      for (int L = 0; L < e->nlong; ++L) tot += e->long_cnt[L];
+      if (tot > pl.NKP / pl.waves)
+        return cleanup_fail(MPCQP_E_UNSUPPORTED, "internal: long mat-vec outputs exceed their staging");
+    }
 
     // occupancy (LDS image and VGPRs) -> persistent grid
     int dev = 0, ncu = 0;
