@@ -212,6 +212,21 @@ int mpcqp_analyze(const mpcqp_structure *st, int32_t *perm, int32_t *Lp, int32_t
 int mpcqp_schedule_check(const mpcqp_structure *st, const double *Px, const double *Ax,
                          double sigma, const double *rho_vec, const double *rhs, double *sol,
                          int64_t *model);
+
+/* The same program as a KKT solver with the factorization and the solves apart (host-only,
+ * diagnostics): mpcqp_emu_factor assembles [[P + sigma I, A'], [A, -diag(1/rho)]] from the
+ * scaled values and runs the factorization schedule; mpcqp_emu_solve runs one forward /
+ * diagonal / backward solve on it, rhs and sol [n + m] in the original order.  Bitwise the
+ * device kernel's factorization and solves (tests/test_gpu_hybrid.py); the oracle's hybrid runs
+ * use it in place of QDLDL. */
+typedef struct mpcqp_emu mpcqp_emu;
+int mpcqp_emu_create(const mpcqp_structure *st, mpcqp_emu **out);
+/* another solver state on the same compiled program (shared, read-only) */
+int mpcqp_emu_clone(const mpcqp_emu *src, mpcqp_emu **out);
+int mpcqp_emu_destroy(mpcqp_emu *e);
+int mpcqp_emu_factor(mpcqp_emu *e, const double *Px, const double *Ax, double sigma,
+                     const double *rho_vec);
+int mpcqp_emu_solve(mpcqp_emu *e, const double *rhs, double *sol);
 /* Host-side export of the symbolic analysis for white-box tests (no device work):
  * perm [n+m] (KKT position -> original KKT index), Lp [n+m+1], Li [nnzL]. */
 int mpcqp_export_symbolic(const mpcqp_handle *h, int32_t *perm, int32_t *Lp, int32_t *Li);

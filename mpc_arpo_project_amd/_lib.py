@@ -25,7 +25,8 @@ EXPORTED = (
     "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",
     "mpcqp_update_bounds", "mpcqp_update_A", "mpcqp_update_lin_cost", "mpcqp_warm_start",
     "mpcqp_solve", "mpcqp_data_buffers", "mpcqp_copy_data", "mpcqp_set_skip", "mpcqp_set_order", "mpcqp_get_state", "mpcqp_set_state", "mpcqp_get_scaling", "mpcqp_dims", "mpcqp_schedule_info", "mpcqp_analyze", "mpcqp_export_symbolic",
-    "mpcqp_schedule_check",
+    "mpcqp_schedule_check", "mpcqp_emu_create", "mpcqp_emu_clone", "mpcqp_emu_destroy", "mpcqp_emu_factor",
+    "mpcqp_emu_solve",
     "mpcqp_status_string", "mpcqp_last_error", "mpcqp_version", "mpcqp_engine_kind", "mpcqp_schedule_kind",
     "mpcqp_kernel_info",
     "mpcqp_cl_create", "mpcqp_cl_destroy", "mpcqp_cl_configure", "mpcqp_cl_step",
@@ -152,6 +153,11 @@ def lib():
     _sig(L, "mpcqp_analyze", "argtypes", [C.POINTER(Structure), i32p, i32p, i32p, i32p, i32p])
     _sig(L, "mpcqp_schedule_check", "argtypes", [C.POINTER(Structure), dp, dp, C.c_double, dp, dp, dp,
                                        C.POINTER(C.c_int64)])
+    _sig(L, "mpcqp_emu_create", "argtypes", [C.POINTER(Structure), C.POINTER(vp)])
+    _sig(L, "mpcqp_emu_clone", "argtypes", [vp, C.POINTER(vp)])
+    _sig(L, "mpcqp_emu_destroy", "argtypes", [vp])
+    _sig(L, "mpcqp_emu_factor", "argtypes", [vp, dp, dp, C.c_double, dp])
+    _sig(L, "mpcqp_emu_solve", "argtypes", [vp, dp, dp])
     _sig(L, "mpcqp_cl_create", "argtypes", [C.POINTER(ClScenario), i32, vp, C.POINTER(vp)])
     _sig(L, "mpcqp_cl_destroy", "argtypes", [vp])
     _sig(L, "mpcqp_cl_configure", "argtypes", [vp, dp, dp, dp, dp])

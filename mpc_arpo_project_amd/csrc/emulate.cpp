@@ -84,10 +84,10 @@ void run_solve_table(const std::vector<uint32_t>& tbl, int nsteps, bool paired, 
 
 }  // namespace
 
-bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, double sigma,
-                       const double* rho_vec, const double* rhs, double* sol) {
+void emulate_factor(const Plan& pl, const double* Px, const double* Ax, double sigma,
+                    const double* rho_vec, std::vector<double>& v) {
   const int n = pl.n, m = pl.m;
-  std::vector<double> v((size_t)pl.LDS_N + 8, std::numeric_limits<double>::quiet_NaN());
+  v.assign((size_t)pl.LDS_N + 8, std::numeric_limits<double>::quiet_NaN());
   // assembly (engine.hip assemble_and_factor)
   for (int k = 0; k < pl.nnzL; ++k) v[pl.LX + k] = 0.0;
   for (int k = 0; k < pl.NKP; ++k) v[pl.DINV + k] = 0.0;
@@ -101,6 +101,10 @@ bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, doubl
   run_fac_table(pl.fac, pl.nfac, v);
   for (int k = 0; k < pl.nnzL; ++k) v[pl.LX + k] *= v[pl.Lcol[k]];
   if (pl.ntail > 0) run_fac_table(pl.tail, pl.ntail, v);
+}
+
+bool emulate_solve(const Plan& pl, std::vector<double>& v, const double* rhs, double* sol) {
+  const int n = pl.n, m = pl.m;
   // one solve (the ADMM loop's vector passes around run_body(fwd) and run_body(bwd))
   // right-hand side into C; W gets it on the copy rows and 0 elsewhere (every W slot is some
   // lane's register-slot slot)
@@ -137,6 +141,13 @@ bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, doubl
   for (int i = n; i < 64 * pl.RN; ++i) finite = finite && v[pl.wsx[i]] == 0.0;
   for (int i = m; i < 64 * pl.RM; ++i) finite = finite && v[pl.wsz[i]] == 0.0;
   return finite;
+}
+
+bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, double sigma,
+                       const double* rho_vec, const double* rhs, double* sol) {
+  std::vector<double> v;
+  emulate_factor(pl, Px, Ax, sigma, rho_vec, v);
+  return emulate_solve(pl, v, rhs, sol);
 }
 
 }  // namespace mpcqp

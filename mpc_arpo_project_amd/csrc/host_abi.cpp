@@ -6,6 +6,7 @@
 // the sanitizer check of the host code (tests/test_sanitize.py).
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <string>
 
 #include "host_abi.hpp"
@@ -137,6 +138,54 @@ int mpcqp_schedule_check(const mpcqp_structure* st, const double* Px, const doub
   }
   if (!emulate_kkt_solve(pl, Px, Ax, sigma, rho_vec, rhs, sol))
     return set_error(MPCQP_E_INVALID, "schedule emulation produced a non-finite or unzeroed slot, or changed a 1/D slot");
+  return 0;
+}
+
+// The compiled device program's factorization and solves on the CPU, factor and solve apart (a
+// KKT solver for the oracle's hybrid parity runs: tests/sweep_parity.py, DESIGN.md Parity)
+struct mpcqp_emu {
+  std::shared_ptr<const Plan> pl;  // shared by clones (read-only)
+  std::vector<double> v;
+  bool factored = false;
+};
+
+int mpcqp_emu_create(const mpcqp_structure* st, mpcqp_emu** out) {
+  if (!st || !out) return set_error(MPCQP_E_INVALID, "null argument");
+  *out = nullptr;
+  auto pl = std::make_shared<Plan>();
+  if (!plan_for(st, *pl)) return set_error(MPCQP_E_UNSUPPORTED, pl->error);
+  mpcqp_emu* e = new mpcqp_emu();
+  e->pl = pl;
+  *out = e;
+  return 0;
+}
+
+int mpcqp_emu_clone(const mpcqp_emu* src, mpcqp_emu** out) {
+  if (!src || !out) return set_error(MPCQP_E_INVALID, "null argument");
+  mpcqp_emu* e = new mpcqp_emu();
+  e->pl = src->pl;
+  *out = e;
+  return 0;
+}
+
+int mpcqp_emu_destroy(mpcqp_emu* e) {
+  delete e;
+  return 0;
+}
+
+int mpcqp_emu_factor(mpcqp_emu* e, const double* Px, const double* Ax, double sigma,
+                     const double* rho_vec) {
+  if (!e || !Px || !Ax || !rho_vec) return set_error(MPCQP_E_INVALID, "null argument");
+  emulate_factor(*e->pl, Px, Ax, sigma, rho_vec, e->v);
+  e->factored = true;
+  return 0;
+}
+
+int mpcqp_emu_solve(mpcqp_emu* e, const double* rhs, double* sol) {
+  if (!e || !rhs || !sol) return set_error(MPCQP_E_INVALID, "null argument");
+  if (!e->factored) return set_error(MPCQP_E_NODATA, "solve before factor");
+  // a non-finite solution is returned as computed (ADMM on an infeasible problem may diverge)
+  (void)emulate_solve(*e->pl, e->v, rhs, sol);
   return 0;
 }
 

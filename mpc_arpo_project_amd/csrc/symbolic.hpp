@@ -265,6 +265,11 @@ void optimize_lds(Plan& pl);
 // factorization schedule, the flat pass, the tail, then one forward / diagonal / backward solve of
 // K [x; nu] = rhs (n + m, original order); writes sol (n + m).  Atomic additions are applied in
 // lane order (the device's order within one instruction may differ: rounding only).
+// the same in two parts: assembly + factorization into the LDS image v, then one solve on it (v's
+// W / C regions are rewritten by every solve; the factor is kept)
+void emulate_factor(const Plan& pl, const double* Px, const double* Ax, double sigma,
+                    const double* rho_vec, std::vector<double>& v);
+bool emulate_solve(const Plan& pl, std::vector<double>& v, const double* rhs, double* sol);
 bool emulate_kkt_solve(const Plan& pl, const double* Px, const double* Ax, double sigma,
                        const double* rho_vec, const double* rhs, double* sol);
 

@@ -101,6 +101,10 @@ def lib():
         L.oqp_set_jitter.restype = None
         L.oqp_set_solve_order.argtypes = [vp, C.c_int]
         L.oqp_set_solve_order.restype = None
+        L.oqp_set_kkt_hook.argtypes = [vp, vp, vp, vp]
+        L.oqp_set_kkt_hook.restype = C.c_int
+        L.oqp_set_fused_updates.argtypes = [vp, C.c_int]
+        L.oqp_set_fused_updates.restype = None
         _lib = L
     return _lib
 
@@ -176,6 +180,17 @@ class OracleOSQP:
         """parity-floor diagnostics: seed != 0 moves every KKT right-hand side entry by one ulp
         (random direction, deterministic per seed) before each solve of the ADMM loop"""
         lib().oqp_set_jitter(self._w, int(seed))
+
+    def set_kkt_hook(self, factor_fn, solve_fn, ctx):
+        """hybrid parity runs: an external KKT factorization + solve (C function pointers and their
+        context, e.g. libmpcqp's mpcqp_emu_factor / mpcqp_emu_solve on an mpcqp_emu) in place of
+        QDLDL's; factors the current data at once.  None removes it."""
+        if lib().oqp_set_kkt_hook(self._w, factor_fn, solve_fn, ctx):
+            raise RuntimeError("oqp_set_kkt_hook: the external factorization failed")
+
+    def set_fused_updates(self, on: bool = True):
+        """hybrid parity runs: the engine's fused ADMM updates (oqp_set_fused_updates)"""
+        lib().oqp_set_fused_updates(self._w, 1 if on else 0)
 
     def set_solve_order(self, order: int):
         """parity-floor diagnostics: 1 / 2 = the KKT solves with every entry's products summed apart

@@ -546,6 +546,13 @@ struct oqp_work {
   double obj_val, pri_res, dua_res;
   /* parity-floor diagnostics only (oqp_set_jitter): xorshift state, 0 = off */
   unsigned long long jitter;
+  /* hybrid parity runs only (oqp_set_kkt_hook): an external KKT factorization + solve in place of
+   * QDLDL's, and the engine's fused updates (oqp_set_fused_updates) */
+  oqp_kkt_factor_fn hook_factor;
+  oqp_kkt_solve_fn hook_solve;
+  void *hook_ctx;
+  double *hook_sol;
+  int fused;
 };
 
 /* scaling.c scale_data */
@@ -637,6 +644,7 @@ static void set_rho_vec(oqp_work *w) {
 }
 
 static int refactor(oqp_work *w) {
+  if (w->hook_factor) return w->hook_factor(w->hook_ctx, w->P->x, w->A->x, w->set.sigma, w->rho_vec);
   return kkt_fill_factor(w->kkt, w->P, w->A, w->set.sigma, w->rho_inv_vec);
 }
 
@@ -762,7 +770,7 @@ void oqp_cleanup(oqp_work *w) {
   free(w->E_temp), free(w->x), free(w->y), free(w->z), free(w->xz_tilde), free(w->x_prev);
   free(w->z_prev), free(w->Ax), free(w->Px), free(w->Aty), free(w->delta_y), free(w->Atdelta_y);
   free(w->delta_x), free(w->Pdelta_x), free(w->Adelta_x), free(w->rho_vec), free(w->rho_inv_vec);
-  free(w->constr_type), free(w->sol_x), free(w->sol_y);
+  free(w->constr_type), free(w->sol_x), free(w->sol_y), free(w->hook_sol);
   kkt_free(w->kkt);
   free(w);
 }
@@ -832,8 +840,21 @@ int oqp_warm_start(oqp_work *w, const double *x, const double *y) {
 static void update_xz_tilde(oqp_work *w) {
   int n = w->n, m = w->m;
   kkt_sys *s = w->kkt;
-  for (int i = 0; i < n; i++) w->xz_tilde[i] = w->set.sigma * w->x_prev[i] - w->q[i];
-  for (int i = 0; i < m; i++) w->xz_tilde[n + i] = w->z_prev[i] - w->rho_inv_vec[i] * w->y[i];
+  if (w->fused) { /* the engine's right-hand side: one rounding per entry (engine.hip) */
+    for (int i = 0; i < n; i++) w->xz_tilde[i] = fma(w->set.sigma, w->x_prev[i], -w->q[i]);
+    for (int i = 0; i < m; i++) w->xz_tilde[n + i] = fma(-w->rho_inv_vec[i], w->y[i], w->z_prev[i]);
+  } else {
+    for (int i = 0; i < n; i++) w->xz_tilde[i] = w->set.sigma * w->x_prev[i] - w->q[i];
+    for (int i = 0; i < m; i++) w->xz_tilde[n + i] = w->z_prev[i] - w->rho_inv_vec[i] * w->y[i];
+  }
+  if (w->hook_solve) { /* the external solver works in the original order: [x~; nu] */
+    w->hook_solve(w->hook_ctx, w->xz_tilde, w->hook_sol);
+    for (int i = 0; i < n; i++) w->xz_tilde[i] = w->hook_sol[i];
+    for (int i = 0; i < m; i++)
+      w->xz_tilde[n + i] = w->fused ? fma(w->rho_inv_vec[i], w->hook_sol[n + i], w->xz_tilde[n + i])
+                                    : w->xz_tilde[n + i] + w->rho_inv_vec[i] * w->hook_sol[n + i];
+    return;
+  }
   /* qdldl_interface solve (non-polish): permute, solve, copy x~, z~ = b_z + rho^-1 nu */
   for (int k = 0; k < s->nk; k++) s->bp[k] = w->xz_tilde[s->perm[k]];
   if (w->jitter) {
@@ -858,7 +879,8 @@ static void update_xz_tilde(oqp_work *w) {
 static void update_x(oqp_work *w) {
   double a = w->set.alpha;
   for (int i = 0; i < w->n; i++) {
-    w->x[i] = a * w->xz_tilde[i] + (1.0 - a) * w->x_prev[i];
+    w->x[i] = w->fused ? fma(a, w->xz_tilde[i], (1.0 - a) * w->x_prev[i])
+                       : a * w->xz_tilde[i] + (1.0 - a) * w->x_prev[i];
     w->delta_x[i] = w->x[i] - w->x_prev[i];
   }
 }
@@ -867,7 +889,8 @@ static void update_z(oqp_work *w) {
   double a = w->set.alpha;
   int n = w->n;
   for (int i = 0; i < w->m; i++) {
-    double v = a * w->xz_tilde[n + i] + (1.0 - a) * w->z_prev[i] + w->rho_inv_vec[i] * w->y[i];
+    double v = w->fused ? fma(w->rho_inv_vec[i], w->y[i], fma(a, w->xz_tilde[n + i], (1.0 - a) * w->z_prev[i]))
+                        : a * w->xz_tilde[n + i] + (1.0 - a) * w->z_prev[i] + w->rho_inv_vec[i] * w->y[i];
     w->z[i] = dmin(dmax(v, w->l[i]), w->u[i]);
   }
 }
@@ -876,8 +899,9 @@ static void update_y(oqp_work *w) {
   double a = w->set.alpha;
   int n = w->n;
   for (int i = 0; i < w->m; i++) {
-    w->delta_y[i] = w->rho_vec[i] *
-                    (a * w->xz_tilde[n + i] + (1.0 - a) * w->z_prev[i] - w->z[i]);
+    const double zr = w->fused ? fma(a, w->xz_tilde[n + i], (1.0 - a) * w->z_prev[i])
+                               : a * w->xz_tilde[n + i] + (1.0 - a) * w->z_prev[i];
+    w->delta_y[i] = w->rho_vec[i] * (zr - w->z[i]);
     w->y[i] += w->delta_y[i];
   }
 }
@@ -1239,6 +1263,17 @@ void oqp_get_y(const oqp_work *w, double *y) { memcpy(y, w->sol_y, sizeof(double
 /* parity-floor diagnostics: order 1 / 2 = the ADMM's KKT solves with every entry's products summed
  * apart (qdldl_solve_sum), 0 = QDLDL's order */
 void oqp_set_solve_order(oqp_work *w, int order) { w->kkt->solve_order = order; }
+
+int oqp_set_kkt_hook(oqp_work *w, oqp_kkt_factor_fn factor, oqp_kkt_solve_fn solve, void *ctx) {
+  free(w->hook_sol);
+  w->hook_sol = NULL;
+  w->hook_factor = factor, w->hook_solve = solve, w->hook_ctx = ctx;
+  if (!factor) return 0;
+  w->hook_sol = (double *)calloc((size_t)(w->n + w->m), sizeof(double));
+  return refactor(w); /* the current scaled data and rho */
+}
+
+void oqp_set_fused_updates(oqp_work *w, int on) { w->fused = on ? 1 : 0; }
 
 /* parity-floor diagnostics: seed != 0 turns on the one-ulp right-hand-side jitter of every KKT
  * solve (update_xz_tilde), with a deterministic per-solver stream; 0 turns it off */

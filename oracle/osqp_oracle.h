@@ -74,6 +74,19 @@ void oqp_set_jitter(oqp_work *w, unsigned long long seed);
  * subtracted once (order 1: backward sums in descending, 2: ascending row order; 0: QDLDL's) */
 void oqp_set_solve_order(oqp_work *w, int order);
 
+/* hybrid parity runs only: an external KKT factorization (scaled upper-P values, A values,
+ * sigma, rho_vec: the matrix [[P + sigma I, A'], [A, -diag(1/rho)]]) and solve (rhs, sol [n + m]
+ * in the original order) in place of QDLDL's -- the engine's compiled device program on the CPU
+ * (libmpcqp's mpcqp_emu_*).  Factors the current data at once; NULL removes it.  Nonzero = error. */
+typedef int (*oqp_kkt_factor_fn)(void *ctx, const double *Px, const double *Ax, double sigma,
+                                 const double *rho_vec);
+typedef int (*oqp_kkt_solve_fn)(void *ctx, const double *rhs, double *sol);
+int oqp_set_kkt_hook(oqp_work *w, oqp_kkt_factor_fn factor, oqp_kkt_solve_fn solve, void *ctx);
+/* hybrid parity runs only: the engine's fused ADMM updates (one rounding per fma: the right-hand
+ * side sigma x - q and z - rho^-1 y, z~ = nu rho^-1 + b_z, the relaxations alpha x~ + (1 - alpha) x
+ * and of z, and z + rho^-1 y) instead of OSQP's separately rounded products */
+void oqp_set_fused_updates(oqp_work *w, int on);
+
 /* results of the last solve */
 void oqp_get_x(const oqp_work *w, double *x);
 void oqp_get_y(const oqp_work *w, double *y);

@@ -32,6 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="radial20", choices=sorted(CASES))
     ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--hybrid-only", action="store_true",
+                    help="the oracle run, the engine run and the two hybrid runs only (no floor draws)")
     a = ap.parse_args()
     scen, nx, noise, rej, tf = CASES[a.case]
     sim, prob = sweep.build(scen, nx, noise, rej, tf)
@@ -42,12 +44,26 @@ def main():
     print(f"oracle run: {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     eng = spp.compare(spp.engine_run(prob, X0, nsim, sim.suc_cond, noise, 1e-3), orc)
     print(f"engine: {time.time() - t0:.1f} s {eng['same_run']}", file=sys.stderr, flush=True)
+    # the hybrid runs (round 6): the oracle with the engine's KKT factorization and blocked solves
+    # (1), and with the engine's fused ADMM updates as well (2: the engine's arithmetic, bitwise --
+    # tests/test_gpu_hybrid.py); which of the two differences moves the loops
+    hyb = {}
+    for h in (1, 2):
+        hyb[h] = spp.compare(spp.oracle_run(prob, X0, nsim, sim.suc_cond, noise, 1e-3, hybrid=h), orc)
+        print(f"hybrid {h}: {time.time() - t0:.1f} s {hyb[h]['same_run']}", file=sys.stderr, flush=True)
+    if a.hybrid_only:
+        print(json.dumps({"case": a.case, "n": a.n, "engine": {k: eng[k] for k in KEYS},
+                          "hybrid_solves": {k: hyb[1][k] for k in KEYS},
+                          "hybrid_solves_fused": {k: hyb[2][k] for k in KEYS}}, indent=1))
+        return
     draws = []
     for d in range(spp.FLOOR_DRAWS):
         draws.append(spp.compare(spp.floor_run(prob, X0, nsim, sim.suc_cond, noise, 1e-3, d), orc))
         print(f"floor draw {d}: {time.time() - t0:.1f} s {draws[-1]['same_run']}", file=sys.stderr,
               flush=True)
     out = {"case": a.case, "n": a.n, "engine": {k: eng[k] for k in KEYS},
+           "hybrid_solves": {k: hyb[1][k] for k in KEYS},
+           "hybrid_solves_fused": {k: hyb[2][k] for k in KEYS},
            "draws": [{k: d[k] for k in KEYS} for d in draws], "summary": {}}
     for k in KEYS:
         v = [d[k] for d in draws]
