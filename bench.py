@@ -397,7 +397,10 @@ def bench_discrete(args, rank, world, device, dist):
                         f"CW scenario, N=Nx={args.nx}, Nc=Nb=5, planar 4-state/2-input "
                         f"{'impulsive delta-v ' if args.dv else ''}model + 5 "
                         f"slacks + 2 disturbances (n={dims['n']}, m={dims['m']}), OSQP 0.6 "
-                        f"settings with eps_abs=eps_rel={args.eps:g}",
+                        f"settings with eps_abs=eps_rel={args.eps:g}; chasers start at rest at "
+                        f"SURVEY 8(d)'s sampled positions (velocities 0 as the reference's x0, no "
+                        f"disturbance estimate: noise=None; the cold parity fixtures use the full "
+                        f"generator)",
             "batch_per_gpu": B,
             "global_batch": world * B,
             "N": args.nx,
@@ -487,6 +490,7 @@ def bench_leg(args, rank, device, nx, dv, batch=None, split=None, label=None):
     model = "impulsive delta-v" if dv else "continuous acceleration"
     return {"metric": f"MPC-QP solves/sec @ N={nx}, {model}, CW, batch={B}; ADMM iters to "
                       f"{args.eps:g}" + (f" ({label})" if label else ""),
+            "initial_states": "at rest at SURVEY 8(d)'s sampled positions (noise=None)",
             "value": float(act.sum()) / run["elapsed"], "unit": "solves/s", "steps": K,
             "warmup": W, "ms_per_step": run["elapsed"] / K * 1e3,
             "config": {"workload": f"warm closed-loop MPC-QP solves, radial CW scenario, N=Nx={nx}, "

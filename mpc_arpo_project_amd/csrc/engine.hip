@@ -1396,11 +1396,7 @@ __device__ __forceinline__ void scale_problem(const KParams& p, int inst, const 
   double cprev = 1.0;  // cost factor of the last pass, not yet applied to P's values
   double dpc[RN];      // P's column norms before that factor (the cost normalisation's)
   LDS_FENCE();
-#ifdef MPCQP_ABL_NOSCALE  // fixed-work ablation builds only
-  for (int it = 0; it < 0; ++it) {
-#else
   for (int it = 0; it < p.s.scaling; ++it) {
-#endif
     // (4, 8) bucket: the passes' operand addresses recomputed in every pass (hoisted out of the
     // pass loop they held ~190 registers: that kernel's register peak, MPCQP_MAX_KERNEL_REGS)
     if constexpr (RN >= 4) {
@@ -1621,9 +1617,7 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
   set_rho(S);
   T_BEGIN(t_f0);
   MatRegs M;  // KM_MREG: the solve steps' matrix operands of the current factorization
-#ifndef MPCQP_ABL_NOFAC  // fixed-work ablation builds only
   assemble_and_factor<RN, RM>(p, sb, v, mv, lane, S);
-#endif
   if constexpr (MREG) {
     LDS_FENCE();
     load_mats(P.fwdm, P.nfwd, (uint32_t)lane, v, M.m[0]);
@@ -1766,19 +1760,15 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     for (int r = 0; r < RN; ++r) {
       xp[r] = S.x[r];
       const double b = fma(sigma, xp[r], -S.q[r]);
-#ifndef MPCQP_ABL_NORHS  // fixed-work ablation builds only (Where the time goes)
       v[wsx[r] + coff] = b;
       v[wsx[r]] = and_d(b, slot_mask(wmk, wbits, r));
-#endif
     }
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       zp[r] = S.z[r];
       bz[r] = fma(-rinv_of(S, r), S.y[r], zp[r]);
-#ifndef MPCQP_ABL_NORHS
       v[wsz[r] + coff] = bz[r];
       v[wsz[r]] = and_d(bz[r], slot_mask(wmk, wbits, RN + r));
-#endif
     }
     LDS_FENCE();
     T_END(T_VEC, t_v0);
@@ -1796,7 +1786,6 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
       prefetch_c(rs_bwd, P.nbwd, (uint32_t)lane, spc);
     else
       prefetch(rs_bwd, P.nbwd, (uint32_t)lane, sp);
-#ifndef MPCQP_ABL_NODIAG
     {
       // C = (1/D) W; W restarts at 0, or at C where the row's identity term is folded into it
       // (Plan::bcopy: the backward task has no MONE term)
@@ -1816,7 +1805,6 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         v[P.W + lane + 64 * r] = and_d(c, slot_mask(bmk, bbits, r));
       }
     }
-#endif
     LDS_FENCE();
     T_END(T_VEC, t_v1);
     T_END(T_V1, t_v1);
@@ -1833,17 +1821,10 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     // together before any use (otherwise the compiler reuses one register pair for all of them
     // and waits for each read in turn)
     double wx[RN], wz[RM];
-#ifdef MPCQP_ABL_NOUPD  // no solution read-back: the update runs on the previous values
-#pragma unroll
-    for (int r = 0; r < RN; ++r) wx[r] = xp[r];
-#pragma unroll
-    for (int r = 0; r < RM; ++r) wz[r] = zp[r];
-#else
 #pragma unroll
     for (int r = 0; r < RN; ++r) wx[r] = v[wsx[r]];  // the junk slot reads back 0
 #pragma unroll
     for (int r = 0; r < RM; ++r) wz[r] = v[wsz[r]];
-#endif
     __builtin_amdgcn_sched_group_barrier(0x100, RN + RM, 0);
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
@@ -1874,19 +1855,13 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
     // RN = 4 the hoisted addresses spilled to scratch; MPCQP_OPAQUE_LANE_RN above)
     int clane = lane;
     if constexpr (RN >= MPCQP_OPAQUE_LANE_RN) asm volatile("" : "+v"(clane));
-#ifndef MPCQP_FIXED_WORK
     if (can_check || adapt) {
       T_BEGIN(t_rs);
       compute_residuals(p, S, R, sb, v, mv, clane TACC_ARG);
       T_END(T_RESID, t_rs);
       T_COUNT(T_NCHK);
     }
-#endif
     if (can_check) {
-#ifdef MPCQP_FIXED_WORK  // diagnostic builds only: 125 iterations per solve, no termination checks
-      if (iter > 100) break;
-      continue;
-#endif
       T_BEGIN(t_tm);
       status = check_termination(p, S, R, dy, dx, sb, v, mv, clane, false TACC_ARG);
       T_END(T_TERM, t_tm);
@@ -2012,19 +1987,6 @@ __global__ void __launch_bounds__(64, KM == KM_MVG ? 2 : MPCQP_WAVES_PER_EU) qp_
   if ((uint32_t)(uintptr_t)lds != 0u) __builtin_trap();  // schedule byte addresses assume base 0
   double* v = lds;
   double* scr = p.scratch + (size_t)blockIdx.x * slab_doubles(p.pl);
-#ifdef MPCQP_PAD_AGPR
-  // diagnostic builds only (the > 190-AGPR shard-overlap cliff): MPCQP_PAD_AGPR extra
-  // accumulation registers held live across the whole kernel, nothing else changed
-#ifndef MPCQP_PAD_KIND
-#define MPCQP_PAD_KIND "+a"  // "+v": the pad in arch VGPRs instead
-#endif
-  uint32_t pad[MPCQP_PAD_AGPR];
-#pragma unroll
-  for (int k = 0; k < MPCQP_PAD_AGPR; ++k) {
-    pad[k] = (uint32_t)k * 2654435761u + (uint32_t)threadIdx.x;
-    asm volatile("" : MPCQP_PAD_KIND(pad[k]));
-  }
-#endif
   for (;;) {
     unsigned int inst = 0;
     if (lane == 0) inst = atomicAdd(p.counter, 1u);
@@ -2043,15 +2005,6 @@ __global__ void __launch_bounds__(64, KM == KM_MVG ? 2 : MPCQP_WAVES_PER_EU) qp_
     solve_instance<RN, RM, PAIRED, KM>(p, (int)inst, v, scr, ilane);
     LDS_FENCE();
   }
-#ifdef MPCQP_PAD_AGPR
-  uint32_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < MPCQP_PAD_AGPR; ++k) {
-    asm volatile("" : MPCQP_PAD_KIND(pad[k]));
-    acc ^= pad[k];
-  }
-  if (acc == 0x12345678u && p.timing) p.timing[0] = acc;  // keeps the pad live; never true in practice
-#endif
 }
 
 // record sets in flight of the two-wave kernel's first wave (Pipe; MPCQP_PAIR_PIPE=3 for A/B)

@@ -1406,7 +1406,11 @@ bool build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
   if (pl.waves == 2) {  // the two-wave kernel's exchange slots and the handed-over instance id
     pl.XCH = pl.LDS_N;
     pl.XID = pl.XCH + XCH_DOUBLES;
+#ifdef MPCQP_PAIR_CHECKS
+    pl.LDS_N = (pl.XID + 4) & ~1;  // + the checked barrier's counters (engine_pair.inc bar2_checked)
+#else
     pl.LDS_N = (pl.XID + 2) & ~1;
+#endif
   }
   if (pl.LDS_N * 8 > (int)META_TGT_MASK || pl.LDS_N >= 65535) {
     pl.error = "LDS image too large for the resident matrix values";
