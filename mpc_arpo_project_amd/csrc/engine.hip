@@ -1112,7 +1112,7 @@ __device__ __forceinline__ void compute_residuals(const KParams& p, Inst<RN, RM>
     ell_apply(P.eAt, tT, mv, yb, R.Aty, lane, v + P.CACC);
   }
   TSYNC(R.Aty[0]);
-  T_END(T_RS3, t_r3);
+  T_END(T_RS1, t_r1);  // the three mat-vecs together (slot rs_matvecs)
   T_BEGIN(t_r4);
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
@@ -1890,12 +1890,17 @@ __device__ __forceinline__ void solve_instance(const KParams& p, int inst, doubl
         tacc[T_FACTOR] += dt_f1;
         tacc[T_CHECK] -= dt_f1;  // the check slot excludes the refactorization
         tacc[T_ADAPT] -= dt_f1;
+        tacc[T_RS2] -= dt_f1;
 #endif
         T_COUNT(T_NFACT);
       }
     }
     T_END(T_ADAPT, t_ad);
     T_END(T_CHECK, t_ck);
+#ifdef MPCQP_TIMING
+    // the check slot split: iterations that run the residuals (check or rho adaptation) / the rest
+    tacc[(can_check || adapt) ? T_RS2 : T_RS3] += __builtin_amdgcn_s_memtime() - t_ck;
+#endif
   }
   T_BEGIN(t_tl);
   if (!can_check) {

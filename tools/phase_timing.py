@@ -15,7 +15,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.environ.get("MPCQP_TIMING_LIB") or os.path.join(REPO, "tools", "libmpcqp_timing.so")
 SLOTS = ["scale", "factor", "fwd", "bwd", "vec", "check", "tail", "iters", "nfact", "resid", "term", "nchk", "adapt",
-         "scale_finish", "vec_rhs", "vec_diag", "vec_update", "rs_stage", "rs_Ax", "rs_Px", "rs_Aty", "rs_norms", "tm_norms", "tm_pinf", "tm_dinf",
+         "scale_finish", "vec_rhs", "vec_diag", "vec_update", "rs_stage", "rs_matvecs", "chk_on", "chk_off", "rs_norms", "tm_norms", "tm_pinf", "tm_dinf",
          "sc_norms", "sc_factors", "sc_rescale", "sc_cost", "sc_cost_seq_count"]
 
 
@@ -76,6 +76,10 @@ def run(B=65536, steps=5, warmup=3, nx=20, dv=0):
                                 "adapt": t["adapt"] / max(t["nchk"], 1),
                                 "check_total": t["check"] / max(t["nchk"], 1),
                                 **{k: t[k] / max(t["nchk"], 1) for k in SLOTS if k.startswith(("rs_", "tm_"))}},
+           # the check slot on the iterations that compute residuals (per such iteration) and on the
+           # others (per iteration): the second is the branch + the stamps' own cost
+           "check_slot_split": {"per_check_iteration": t["chk_on"] / max(t["nchk"], 1),
+                                "per_other_iteration": t["chk_off"] / max(iters - t["nchk"], 1)},
            "scale_finish_per_solve": t["scale_finish"] / n_inst,
            # the Ruiz passes' parts, per pass (scaling passes per solve = settings.scaling, 10)
            "ruiz_cycles_per_pass": {k: t[k] / (10 * n_inst) for k in ("sc_norms", "sc_factors",
