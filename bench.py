@@ -316,6 +316,14 @@ def roofline(run, S, K, elapsed):
                     "fraction is claimed from it (the measured HBM figure is `hbm`)"})
 
 
+def _sources_match(pj):
+    """True when the committed profile was measured on a library built from exactly this tree's
+    sources (its src_digest, _lib.source_digest); None for profiles that predate the digest"""
+    from mpc_arpo_project_amd._lib import source_digest
+
+    return None if "src_digest" not in pj else pj["src_digest"] == source_digest()
+
+
 def attach_profiles(roof, B, nx, S, K, elapsed, dv=False, kind="discrete"):
     """HBM traffic (PMC FETCH_SIZE + WRITE_SIZE) and LDS busy share (SQ_LDS_IDX_ACTIVE) from the
     committed profile of this workload, when there is one."""
@@ -328,6 +336,7 @@ def attach_profiles(roof, B, nx, S, K, elapsed, dv=False, kind="discrete"):
                        "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": t,
                        "bytes_per_solve": pj.get("hbm_bytes_per_solve"),
                        "measured_at": pj.get("commit"),
+                       "sources_match": _sources_match(pj),
                        "what": "PMC FETCH_SIZE + WRITE_SIZE (L2 <-> fabric, calibrated; "
                                "tools/pmc_run.sh)"}
     sq = load_profile("sq_summary.json", B, nx, S, dv, kind)
@@ -335,6 +344,7 @@ def attach_profiles(roof, B, nx, S, K, elapsed, dv=False, kind="discrete"):
         roof["lds_busy"] = {"frac": sq["lds_array_busy_fraction_if_per_cu"],
                             "bank_conflict_share": sq.get("lds_conflict_share"),
                             "measured_at": sq.get("commit"),
+                            "sources_match": _sources_match(sq),
                             "what": "SQ_LDS_IDX_ACTIVE / CU cycles of the solve kernel (all LDS-"
                                     "array cycles, atomics at their real cost; tools/pmc_sq.sh)"}
 

@@ -20,6 +20,26 @@ if os.environ.get("MPCQP_LIBRARY") and not _DIAG:
                        "load only under MPCQP_DIAGNOSTICS=1")
 LIB_PATH = (_DIAG and os.environ.get("MPCQP_LIBRARY")) or os.path.join(_HERE, "libmpcqp.so")
 
+
+
+def source_digest():
+    """First 12 hex digits of a sha256 over the sources libmpcqp.so is built from (csrc/ and
+    include/, sorted by name).  tools/profile_post.py stamps it into the committed profiles and
+    bench.py compares it with the tree it runs from, so a profile is matched to the benched build
+    by content, not only by the commit it was measured at."""
+    import hashlib
+
+    h = hashlib.sha256()
+    repo = os.path.dirname(_HERE)
+    for d in (os.path.join(_HERE, "csrc"), os.path.join(repo, "include")):
+        for f in sorted(os.listdir(d)):
+            if f.endswith((".hip", ".cpp", ".hpp", ".inc", ".h")):
+                h.update(f.encode())
+                with open(os.path.join(d, f), "rb") as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
 # every symbol include/mpcqp.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "mpcqp_default_settings", "mpcqp_create", "mpcqp_destroy", "mpcqp_set_data",

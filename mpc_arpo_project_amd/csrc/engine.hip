@@ -2514,6 +2514,14 @@ int mpcqp_debug_timing(mpcqp_handle* h, unsigned long long* dev_buf) {
 }
 #endif
 
+#ifdef MPCQP_PAIR_CHECKS
+// diagnostic builds only (not part of include/mpcqp.h): arm / disarm the injected barrier skip of
+// the two-wave kernel (g_pair_inject) for the following launches
+int mpcqp_debug_pair_inject(int on) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_pair_inject), &on, sizeof(int)) == hipSuccess ? 0 : MPCQP_E_HIP;
+}
+#endif
+
 int mpcqp_data_buffers(mpcqp_handle* h, double** Ax, double** l, double** u) {
   if (!h) return fail(MPCQP_E_INVALID, "null handle");
   // the caller may rewrite A in place between solves: every later solve follows an update of A

@@ -2,7 +2,10 @@
 whatever library MPCQP_LIBRARY names (the -DMPCQP_PAIR_CHECKS diagnostic build); the statuses,
 iterations and iterates go to an .npz the parent compares with the product library's.
 
-    python tests/_pair_checks_run.py <Nx> <dv 0|1> <fixture tag> <out.npz>
+    python tests/_pair_checks_run.py <Nx> <dv 0|1> <fixture tag> <out.npz> [inject]
+
+With `inject` the first solve runs with the checks build's barrier skip armed
+(mpcqp_debug_pair_inject: wave 1 of workgroup 0 skips one barrier), the second without it.
 """
 import os
 import sys
@@ -19,6 +22,7 @@ from mpc_arpo_project_amd.engine import BatchQP  # noqa: E402
 
 def main():
     nx, dv, tag, out = int(sys.argv[1]), bool(int(sys.argv[2])), sys.argv[3], sys.argv[4]
+    inject = len(sys.argv) > 5 and sys.argv[5] == "inject"
     prob = problem(nx, dv)
     d = load_golden(tag)
     reps = 8192 // d["Ax"].shape[0]
@@ -27,6 +31,13 @@ def main():
     qp.set_data(q=prob.q, Ax=Ax, l=l, u=u)
     res = {}
     for k in range(2):  # cold, then warm from the first solve's state
+        if inject:
+            import ctypes
+
+            from mpc_arpo_project_amd import _lib
+            f = _lib.lib().mpcqp_debug_pair_inject
+            f.argtypes, f.restype = [ctypes.c_int], ctypes.c_int
+            assert f(1 if k == 0 else 0) == 0
         r = qp.solve()
         res.update({f"status{k}": r.status.cpu().numpy(), f"iter{k}": r.iter.cpu().numpy(),
                     f"x{k}": r.x.cpu().numpy(), f"y{k}": r.y.cpu().numpy()})

@@ -47,6 +47,10 @@ def main():
         "scratch": int(r0["Scratch_Size"]), "workgroup": int(r0["Workgroup_Size_X"]),
         "grid": int(r0["Grid_Size_X"]),
     }
+    # the engine's own figure (hipFuncGetAttributes of the selected kernel, bench schedule)
+    kr = bench.get("schedule", {}).get("kernel_regs")
+    out["schedule_kernel_regs"] = kr
+    out["regs_match"] = None if kr is None else out["unified_regs_allocated"] == kr
     print(json.dumps(out, indent=1))
 
 

@@ -16,6 +16,12 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TOOLS = os.path.join(REPO, "tools")
+sys.path.insert(0, REPO)
+from mpc_arpo_project_amd._lib import source_digest  # noqa: E402
+
+# the sources of the library that was profiled: this tree's (run profile_post on the tree that was
+# pushed to the GPU box, before any source edit)
+SRC_DIGEST = source_digest()
 
 
 def run(args):
@@ -31,7 +37,7 @@ def meta(bench, kind, dv, commit):
     b = json.loads(open(bench).read().strip().splitlines()[-1])
     return {"batch": b["config"]["batch_per_gpu"], "nx": b["config"]["N"],
             "concurrent_shards": b["roofline"].get("concurrent_shards", 1), "dv": dv, "kind": kind,
-            "commit": commit}
+            "commit": commit, "src_digest": SRC_DIGEST}
 
 
 def main():
@@ -51,8 +57,9 @@ def main():
         if not t or not os.path.exists(bj):
             continue
         # the untimed warm-up launches: warmup x concurrent shards (prof_summary's default)
-        out = run([os.path.join(TOOLS, "prof_summary.py"), t, bj])
-        open(os.path.join(a.dst, f"prof_summary{name}.json"), "w").write(out)
+        out = json.loads(run([os.path.join(TOOLS, "prof_summary.py"), t, bj]))
+        out.update(commit=commit, src_digest=SRC_DIGEST)
+        json.dump(out, open(os.path.join(a.dst, f"prof_summary{name}.json"), "w"), indent=1)
         shutil.copy(bj, os.path.join(a.dst, f"bench{name}.json"))
         st = glob.glob(os.path.join(a.src, tdir, "**", "*kernel_stats.csv"), recursive=True)
         if st:
