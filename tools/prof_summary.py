@@ -47,10 +47,23 @@ def main():
         "scratch": int(r0["Scratch_Size"]), "workgroup": int(r0["Workgroup_Size_X"]),
         "grid": int(r0["Grid_Size_X"]),
     }
-    # the engine's own figure (hipFuncGetAttributes of the selected kernel, bench schedule)
+    # per HIP stream (concurrent shards): the continuous-time bench times shard 0's solve only
+    # (period_split_ms), so its figure is compared with the launches on shard 0's stream -- the
+    # stream of the first launch (shard 0 is enqueued first in every period)
+    streams = {}
+    for r, d in zip(rows[warm:], timed):
+        streams.setdefault(r.get("Stream_Id", "0"), []).append(float(d))
+    out["per_stream_ms_per_launch"] = {k: float(np.mean(v)) for k, v in streams.items()}
+    if "period_split_ms" in bench:
+        s0 = rows[0].get("Stream_Id", "0")
+        out["agreement_all_streams"] = out["agreement"]
+        out["agreement"] = float(np.mean(streams[s0]) / bench["roofline"]["kernel_ms_per_launch"])
+        out["agreement_of"] = "shard 0's stream (the bench times shard 0's solve)"
+    # the engine's own figure (hipFuncGetAttributes of the selected kernel, bench schedule); rocprof
+    # reports the allocation in whole granules of 8 registers
     kr = bench.get("schedule", {}).get("kernel_regs")
     out["schedule_kernel_regs"] = kr
-    out["regs_match"] = None if kr is None else out["unified_regs_allocated"] == kr
+    out["regs_match"] = None if kr is None else out["unified_regs_allocated"] == -(-kr // 8) * 8
     print(json.dumps(out, indent=1))
 
 
