@@ -12,8 +12,13 @@ record descriptor in its step loop):
   * the solve-step loops (the record pipelines: three LDS atomics and five record loads per step)
     contain no `v_readlane` (SGPR-spill reload) and no `s_load` (kernel-argument reload);
   * the first block of the ADMM loop (its header up to the first solve's record prefetch) contains
-    no `s_load`.
+    no `s_load`;
+  * (round 6) an ADMM iteration that neither checks nor adapts rho -- the
+    shortest path through the loop, which skips every check block -- reloads no kernel argument
+    and at most the spilled SGPRs it reloads today (the checks' own reloads run once per
+    check_termination iterations and are not capped here).
 """
+import heapq
 import os
 import re
 import subprocess
@@ -98,3 +103,71 @@ def test_admm_loop_head_does_not_reload_kernel_arguments(isa):
                 break
             head.append(t)
         assert not any(t.startswith("s_load") for t in head), (name, head[:12])
+
+
+# v_readlane (SGPR-spill reloads) on a non-check iteration, as built in round 6: the N = 20 kernel
+# 3 (loop counters at the head), the two-wave N = 40 kernel 0, the (4, 8) one-wave kernel 23
+NONCHECK_RELOADS = {"qp_batch_kernelILi2ELi4": 3, "qp_pair_kernelILi2ELi4": 0, "qp_batch_kernelILi4ELi8": 23}
+
+
+def _succ(ins, i, idx):
+    _, t, tgt = ins[i]
+    op = t.split()[0]
+    if op == "s_branch":
+        return [idx[tgt]] if tgt in idx else []
+    if op.startswith("s_cbranch"):
+        return ([idx[tgt]] if tgt in idx else []) + [i + 1]
+    if op in ("s_endpgm", "s_setpc_b64"):
+        return []
+    return [i + 1]
+
+
+def _shortest(ins, idx, a, b, lo, hi):
+    """instruction indices of a shortest path a -> b inside [lo, hi]"""
+    dist, prev, pq = {a: 0}, {}, [(0, a)]
+    while pq:
+        d, i = heapq.heappop(pq)
+        if i == b:
+            break
+        if d > dist.get(i, 1 << 60):
+            continue
+        for j in _succ(ins, i, idx):
+            if lo <= j <= hi and d + 1 < dist.get(j, 1 << 60):
+                dist[j], prev[j] = d + 1, i
+                heapq.heappush(pq, (d + 1, j))
+    path = [b]
+    while path[-1] != a:
+        path.append(prev[path[-1]])
+    return path[::-1]
+
+
+def _step_loops(ins):
+    return [(h, e) for h, e in loops(ins)
+            if e - h < 1500 and sum("ds_add" in t for _, t, _ in ins[h:e + 1]) >= 6
+            and sum("buffer_load" in t for _, t, _ in ins[h:e + 1]) >= 10]
+
+
+def shortest_iteration(ins):
+    """instruction texts of the shortest path from the ADMM loop's header to its back edge through
+    its first two solve-step loops (the forward and backward solves, each run once): an iteration of
+    the solving wave that skips every check block"""
+    idx = {a: i for i, (a, _, _) in enumerate(ins)}
+    h, e = max(loops(ins), key=lambda x: x[1] - x[0])
+    way = [h]
+    for sh, se in sorted(l for l in _step_loops(ins) if h < l[0] and l[1] < e)[:2]:  # fwd, bwd
+        way += [sh, se]
+    way.append(e)
+    path = [h]
+    for a, b in zip(way, way[1:]):
+        path += _shortest(ins, idx, a, b, h, e)[1:]
+    return [ins[i][1] for i in path]
+
+
+def test_non_check_iterations_reload_no_kernel_argument_and_few_spills(isa):
+    for name, ins in isa.items():
+        cap = next(v for k, v in NONCHECK_RELOADS.items() if k in name)
+        path = shortest_iteration(ins)
+        assert sum("ds_add_f64" in t for t in path) >= 6, (name, "not a solving path")
+        assert not any(t.startswith("s_load") for t in path), name
+        reloads = [t for t in path if t.startswith("v_readlane")]
+        assert len(reloads) <= cap, (name, len(reloads), reloads[:6])
